@@ -1,0 +1,172 @@
+/*
+ * orbfe.h — C-ABI of the MI355X-native ORB front-end (liborbfe.so, gfx950 HIP).
+ *
+ * Drop-in boundary for the pyOrbSLAM2 front-end hot path.  Each entry point names the reference
+ * interface it replaces (paths relative to the reference repo M2219/pyOrbSLAM):
+ *
+ *   pyORBExtractor.ORBextractor            pyORBExtractor/orb_extractor.cpp:22-38, ORBextractor.h:45-114
+ *   Frame.compute_stereo_matches           Frame.py:161-279
+ *   ORBMatcher.descriptor_distance / search_by_projection_f_f / _f_p (Hamming core)
+ *                                          ORBMatcher.py:12-14, 215-283, 291-393
+ *
+ * Conventions
+ *   - plain C types only; caller-owned output buffers; every call returns an int status
+ *     (ORBFE_OK = 0, < 0 on error) and the message is kept in a thread-local string
+ *     readable with orbfe_last_error();
+ *   - one handle per camera / per thread (the reference extractor is stateful and not
+ *     re-entrant: ORBextractor.h:88 overwrites mvImagePyramid on every call);
+ *   - "device" entry points take device pointers and a hipStream_t passed as void*;
+ *     they enqueue work and return without synchronising.
+ */
+#ifndef ORBFE_H
+#define ORBFE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBFE_OK 0
+#define ORBFE_EINVAL (-1)    /* bad argument / unsupported configuration            */
+#define ORBFE_ENOMEM (-2)    /* host or device allocation failed                    */
+#define ORBFE_EHIP (-3)      /* HIP runtime error (message from hipGetErrorString)   */
+#define ORBFE_ECAPACITY (-4) /* caller buffer too small (*n_out holds the need)     */
+#define ORBFE_ESTATE (-5)    /* call order violated (e.g. pyramid before extract)   */
+#define ORBFE_EOVERFLOW (-6) /* an on-device capacity bound was exceeded            */
+
+/* ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+ * (orb_extractor.cpp:23; ORBextractor.cpp:410-470). */
+typedef struct orbfe_params {
+    int32_t nfeatures;
+    float scale_factor; /* narrowed to float exactly like the pybind11 float argument */
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    /* Lane count of OpenCV's vectorised vertical resize pass (cv::resize INTER_LINEAR 8U,
+     * SURVEY.md Appendix A.2 / H2): 16 = CV_SIMD128 baseline build (default), 32 = AVX2-wide
+     * build, 0 = scalar formula everywhere.  OpenCV is not vendored by the reference; this is
+     * the only unpinned knob of the pixel arithmetic. */
+    int32_t resize_simd_lanes;
+} orbfe_params;
+
+/* cv::KeyPoint as the reference's caster returns it: (pt.x, pt.y, size, angle, response,
+ * octave) (opencv_type_casters.h:106-108).  24 bytes, naturally aligned. */
+typedef struct orbfe_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave;
+} orbfe_keypoint;
+
+typedef struct orbfe_ctx* orbfe_handle;
+
+/* ---- lifetime ------------------------------------------------------------------------ */
+
+/* ORBextractor::ORBextractor (ORBextractor.cpp:410-470). */
+int orbfe_create(const orbfe_params* params, orbfe_handle* out);
+int orbfe_destroy(orbfe_handle h);
+const char* orbfe_last_error(void);
+/* library build string ("gfx950 ...") */
+const char* orbfe_version(void);
+
+/* GetLevels/GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
+ * GetInverseScaleSigmaSquares (ORBextractor.h:62-82).  Each array has nlevels floats; any
+ * pointer may be NULL.  n_per_level receives mnFeaturesPerLevel (ORBextractor.cpp:435-446). */
+int orbfe_get_scales(orbfe_handle h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                     int32_t* n_per_level);
+
+/* ---- host-buffer drop-in (one image per call) ------------------------------------------ */
+
+/* ORBextractor::operator_kd (ORBextractor.cpp:1042-1104) as bound at orb_extractor.cpp:31-38.
+ * img: width x height u8, row stride `stride` bytes (the reference ignores numpy strides and
+ * requires C-contiguous input; pass stride = width for identical behaviour).
+ * Writes up to `cap` keypoints and cap*32 descriptor bytes; *n_out = number produced.
+ * An empty image (width or height 0) yields *n_out = 0 (ORBextractor.cpp:1045-1046). */
+int orbfe_extract(orbfe_handle h, const uint8_t* img, int32_t width, int32_t height, int32_t stride,
+                  orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out);
+
+/* GetImagePyramid (orb_extractor.cpp:30): pyramid level `level` of the last orbfe_extract.
+ * sheared = 1 reproduces the reference's Mat->ndarray caster, which ignores Mat::step and so
+ * returns row r of a level as bytes [19*(w+38)+19 + r*w, ... + w) of the 19-px reflect-101
+ * padded buffer (opencv_type_casters.h:232-239; ORBextractor.cpp:1112-1128);
+ * sheared = 0 returns the true w x h level.  out must hold w*h bytes (sizes via w_out, h_out;
+ * call with out = NULL to query the size). */
+int orbfe_pyramid(orbfe_handle h, int32_t level, uint8_t* out, int32_t sheared, int32_t* w_out,
+                  int32_t* h_out);
+
+/* Frame.compute_stereo_matches (Frame.py:161-279) on the last left/right extraction of two
+ * handles (left = hl, right = hr; both must have extracted same-size images).
+ * bf = Frame.mbf (Python float), fx = Frame.mK[0][0] (np.float32).
+ * Outputs, each of length nL = number of left keypoints:
+ *   status[i] = 0  no match      (reference keeps Python int -1)
+ *             = 1  matched       (reference stores np.float32 uR / depth: u_right / depth)
+ *             = 2  zero disparity: the reference substitutes disparity = 0.01 in Python double
+ *                  precision (Frame.py:273-275); u_right/depth then hold uL-0.01 and bf/0.01
+ *                  rounded to f32 and the host layer recomputes them in double.
+ *   match_r[i] = index of the right keypoint chosen by the Hamming search (or -1). */
+int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, float* u_right, float* depth,
+                       int8_t* status, int32_t* match_r, int32_t n_left);
+
+/* ---- device batch API (bench / batched-frames mode) ----------------------------------------
+ * Images are device-resident, n_images x (height x img_pitch) u8, stereo pair p = images
+ * (2p, 2p+1) = (left, right).  Results stay on device in handle-owned buffers. */
+
+/* Allocate device workspace for up to max_images images of width x height (idempotent for the
+ * same geometry). */
+int orbfe_batch_reserve(orbfe_handle h, int32_t width, int32_t height, int32_t max_images);
+
+/* Run the whole extractor on n_images device images (no host synchronisation). */
+int orbfe_extract_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t img_pitch, int32_t n_images,
+                               void* hip_stream);
+
+/* Stereo-match n_pairs pairs of the last batch extraction (images 2p, 2p+1). */
+int orbfe_stereo_batch_device(orbfe_handle h, int32_t n_pairs, double bf, float fx, void* hip_stream);
+
+/* Convenience: extract + stereo for n_pairs pairs in one enqueue (the benchmark step). */
+int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t img_pitch, int32_t n_pairs,
+                                double bf, float fx, void* hip_stream);
+
+/* Device result layout of the last batch (pointers into handle-owned device memory):
+ *   kps   : n_images x cap  orbfe_keypoint   (cap = *kp_cap)
+ *   desc  : n_images x cap x 32 u8
+ *   count : n_images int32
+ *   u_right, depth : n_pairs x cap float; status : n_pairs x cap int8; match_r : n_pairs x cap int32 */
+typedef struct orbfe_batch_view {
+    int32_t kp_cap;
+    int32_t n_images;
+    int32_t n_pairs;
+    orbfe_keypoint* kps;
+    uint8_t* desc;
+    int32_t* count;
+    float* u_right;
+    float* depth;
+    int8_t* status;
+    int32_t* match_r;
+    int32_t* overflow; /* device int: non-zero if a capacity bound was hit in the last batch */
+} orbfe_batch_view;
+int orbfe_batch_view_get(orbfe_handle h, orbfe_batch_view* view);
+
+/* Copy the results of image `image` (and of pair image/2 when image is even and a stereo
+ * batch ran) of the last batch to host buffers.  Synchronises the handle's last stream. */
+int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap,
+                      int32_t* n_out);
+
+/* ---- Hamming search (ORBMatcher core) -------------------------------------------------------
+ * ORBMatcher.descriptor_distance (ORBMatcher.py:12-14): popcount(a ^ b) over 32 bytes, batched.
+ * For query q the candidates are cand_idx[cand_off[q] .. cand_off[q+1]) (indices into
+ * train_desc), scanned in order; the search keeps the FIRST strict minimum (best) and the
+ * second-best distance with its candidate exactly as search_by_projection_f_p does
+ * (ORBMatcher.py:252-274: `dist < best` shifts best into second; `elif dist < best2`).
+ * Distances start at 256 (no candidate => best_idx = -1).  Host pointers; n_query may be 0. */
+int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
+                         int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* best_dist,
+                         int32_t* best_idx, int32_t* second_dist, int32_t* second_idx);
+
+/* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
+int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
+                         int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBFE_H */
