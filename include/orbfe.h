@@ -150,6 +150,11 @@ int orbfe_batch_view_get(orbfe_handle h, orbfe_batch_view* view);
 int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap,
                       int32_t* n_out);
 
+/* Copy the stereo results of pair `pair` of the last batch (see orbfe_stereo_match for the meaning
+ * of the arrays; *n_out = left keypoint count of the pair).  Synchronises the last stream. */
+int orbfe_batch_fetch_stereo(orbfe_handle h, int32_t pair, float* u_right, float* depth, int8_t* status,
+                             int32_t* match_r, int32_t cap, int32_t* n_out);
+
 /* ---- Hamming search (ORBMatcher core) -------------------------------------------------------
  * ORBMatcher.descriptor_distance (ORBMatcher.py:12-14): popcount(a ^ b) over 32 bytes, batched.
  * For query q the candidates are cand_idx[cand_off[q] .. cand_off[q+1]) (indices into
@@ -164,6 +169,23 @@ int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_qu
 /* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);
+
+/* ---- live stage timing --------------------------------------------------------------------------
+ * While profiling is on, every batch enqueued on the handle records HIP events on its launch stream
+ * at the stage boundaries: 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree,
+ * 3 describe (IC angle + blur + BRIEF), 4 stereo.  orbfe_profile_read synchronises and returns the
+ * summed milliseconds per stage over the recorded batches. */
+#define ORBFE_NSTAGES 5
+int orbfe_profile_begin(orbfe_handle h, int32_t max_batches);
+int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches);
+
+/* ---- diagnostics (stage outputs of the last orbfe_extract, image 0) ------------------------------
+ * orbfe_debug_candidates: the level's FAST cell output in vToDistributeKeys order
+ *   (ORBextractor.cpp:808-824), as (x_rel, y_rel, score) triples relative to (minBorderX, minBorderY).
+ * orbfe_debug_selected: DistributeOctTree's result for the level in list order
+ *   (ORBextractor.cpp:833-834), as (x_rel, y_rel, score) triples. */
+int orbfe_debug_candidates(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out);
+int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out);
 
 #ifdef __cplusplus
 }

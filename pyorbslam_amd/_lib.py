@@ -1,0 +1,118 @@
+"""ctypes binding of liborbfe.so (the gfx950 C-ABI declared in include/orbfe.h).
+
+The library is built in-tree (make / __graft_entry__.build()) into pyorbslam_amd/_lib/.  There is no
+CPU fallback: if the shared object is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "liborbfe.so"
+
+ORBFE_OK = 0
+ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ESTATE", -6: "EOVERFLOW"}
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("resize_simd_lanes", C.c_int32)]
+
+
+class BatchView(C.Structure):
+    _fields_ = [("kp_cap", C.c_int32), ("n_images", C.c_int32), ("n_pairs", C.c_int32),
+                ("kps", C.c_void_p), ("desc", C.c_void_p), ("count", C.c_void_p), ("u_right", C.c_void_p),
+                ("depth", C.c_void_p), ("status", C.c_void_p), ("match_r", C.c_void_p), ("overflow", C.c_void_p)]
+
+
+# cv::KeyPoint tuple layout (opencv_type_casters.h:106-108)
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4")])
+
+# every symbol include/orbfe.h declares (tests check the export table against the header)
+SIGNATURES = {
+    "orbfe_create": [C.POINTER(Params), C.POINTER(C.c_void_p)],
+    "orbfe_destroy": [C.c_void_p],
+    "orbfe_last_error": [],
+    "orbfe_version": [],
+    "orbfe_get_scales": [C.c_void_p] + [C.c_void_p] * 5,
+    "orbfe_extract": [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
+                      C.POINTER(C.c_int32)],
+    "orbfe_pyramid": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
+    "orbfe_stereo_match": [C.c_void_p, C.c_void_p, C.c_double, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
+                           C.c_void_p, C.c_int32],
+    "orbfe_batch_reserve": [C.c_void_p, C.c_int32, C.c_int32, C.c_int32],
+    "orbfe_extract_batch_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p],
+    "orbfe_stereo_batch_device": [C.c_void_p, C.c_int32, C.c_double, C.c_float, C.c_void_p],
+    "orbfe_frontend_batch_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_float, C.c_void_p],
+    "orbfe_batch_view_get": [C.c_void_p, C.POINTER(BatchView)],
+    "orbfe_batch_fetch": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
+    "orbfe_batch_fetch_stereo": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                 C.POINTER(C.c_int32)],
+    "orbfe_hamming_search": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    "orbfe_hamming_matrix": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p],
+    "orbfe_profile_begin": [C.c_void_p, C.c_int32],
+    "orbfe_profile_read": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],
+    "orbfe_debug_candidates": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
+    "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
+}
+
+_lib: C.CDLL | None = None
+
+
+class OrbfeError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    """Load liborbfe.so (raises OSError if it is missing: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise OSError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()) first; "
+                          "pyorbslam_amd has no CPU fallback")
+        L = C.CDLL(str(LIB_PATH))
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = C.c_char_p if name in ("orbfe_last_error", "orbfe_version") else C.c_int
+        _lib = L
+    return _lib
+
+
+def check(fn: str, rc: int) -> None:
+    if rc != ORBFE_OK:
+        raise OrbfeError(fn, rc, lib().orbfe_last_error().decode(errors="replace"))
+
+
+def call(name: str, *args) -> None:
+    check(name, getattr(lib(), name)(*args))
+
+
+def ptr(a: np.ndarray | None) -> C.c_void_p | None:
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def make_params(nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
+                resize_simd_lanes: int = 16) -> Params:
+    # pybind11 narrows the scaleFactor argument to C++ float (orb_extractor.cpp:23)
+    return Params(int(nfeatures), float(np.float32(scaleFactor)), int(nlevels), int(iniThFAST), int(minThFAST),
+                  int(resize_simd_lanes))
+
+
+def version() -> str:
+    return lib().orbfe_version().decode()
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+        return bool(torch.cuda.is_available())
+    except Exception:  # pragma: no cover
+        return False

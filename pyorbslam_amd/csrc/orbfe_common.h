@@ -1,0 +1,82 @@
+// orbfe_common.h — geometry tables shared by the host setup (orbfe_host.hip) and the gfx950 kernels
+// (orbfe_kernels.hip).  All tables are computed once per (extractor params, image size) on the host
+// with the reference's own float/double arithmetic and uploaded to device memory.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbfe.h"
+
+namespace orbfe {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdge = 19;          // EDGE_THRESHOLD (ORBextractor.cpp:74)
+constexpr int kBorder = kEdge - 3; // minBorderX/Y (ORBextractor.cpp:772-773)
+constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
+constexpr int kPatchR = 21;        // descriptor patch radius: 18 (max rotated pattern offset) + 3 (blur)
+constexpr int kPatchD = 2 * kPatchR + 1;  // 43
+constexpr int kBlurR = 18;
+constexpr int kBlurD = 2 * kBlurR + 1;    // 37
+constexpr int kMaxCellRoi = 64;    // max cell ROI side (wCell+6, hCell+6); checked on the host
+
+// One pyramid level of one image geometry.
+struct LevelGeo {
+    int w, h;            // level size: cvRound(W * invScale), cvRound(H * invScale) (:1110-1111)
+    int64_t ws_off;      // byte offset of the level inside an image's pyramid workspace (levels >= 1)
+    float scale, inv_scale;
+    int n_feat;          // mnFeaturesPerLevel[l]
+    int kp_cap;          // capacity of the per-level selected list: max(N+2, 4*nIni) + 2
+    int kp_off;          // offset of the level inside an image's level-keypoint array
+    float size;          // (float)(int)(PATCH_SIZE * scale) (:836)
+    // DistributeOctTree frame (relative to minBorder): [0, maxX-minX) x [0, maxY-minY)
+    int span_x, span_y;
+    int n_ini;           // round((float)spanX / spanY)
+    float hx;            // (float)spanX / nIni
+    int cell0, ncell;    // first cell (global cell index) and number of cells of this level
+    int key_off;         // offset of the level's dense candidate scratch inside an image
+    int key_cap;         // sum of the level's cell slot capacities
+    // cv::resize tables (levels >= 1): column table at xtab_off (xofs, a0, a1), row table at ytab_off
+    int xtab_off, ytab_off;
+    int xmax;            // first column whose sx+1 >= src width
+    int xvec;            // end of OpenCV's vectorised span of the vertical pass
+    int chunk0;          // first k_describe block of this level (4 keypoints per block)
+};
+
+// One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.
+struct CellGeo {
+    int16_t level, pad;
+    int16_t x0, y0, x1, y1;
+    int slot_off;        // offset (in keys) of the cell's output slot inside an image's slot array
+    int slot_cap;        // ceil(ww/2)*ceil(wh/2): strict 3x3 NMS keeps at most one pixel per 2x2 block
+};
+
+// Resize column entry.
+struct ResizeX {
+    int32_t sx;
+    int16_t a0, a1;
+};
+struct ResizeY {
+    int32_t sy0, sy1;    // already clipped to [0, src_h)
+    int16_t b0, b1;
+};
+
+// Per-geometry constants passed by value to every kernel.
+struct Geo {
+    int nlevels;
+    int W, H;
+    int ncells;
+    int ini_th, min_th;
+    int kp_cap;          // per-image capacity of the final keypoint list (sum of level kp_cap)
+    int lvl_kp_cap;      // per-image size of the level-keypoint array (same as kp_cap)
+    int64_t ws_bytes;    // per-image pyramid workspace bytes (levels >= 1)
+    int64_t slot_total;  // per-image cell slot count
+    int64_t key_total;   // per-image dense candidate scratch count
+    int max_ncap;        // octree node capacity (max over levels of kp_cap)
+    int umax[16];
+    float scale[kMaxLevels];
+    float inv_scale[kMaxLevels];
+    LevelGeo lv[kMaxLevels];
+};
+
+}  // namespace orbfe

@@ -1,0 +1,824 @@
+// orbfe_host.hip — C-ABI (include/orbfe.h) of the gfx950 ORB front-end: extractor handle, geometry
+// tables, device workspace and the enqueue of the kernel pipeline.
+//
+// Host arithmetic that feeds the kernels (scale tables, level sizes, cell grid, resize coefficients) is
+// computed here with the same float/double expressions as the reference (ORBextractor.cpp:410-470,
+// 764-828, 1106-1132; OpenCV resize coefficient setup), so every kernel consumes identical integers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "orbfe_common.h"
+#include "orbfe_kernels.h"
+
+using namespace orbfe;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCK(expr)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            throw Error(ORBFE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return ORBFE_OK;
+    } catch (const Error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "host allocation failed";
+        return ORBFE_ENOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return ORBFE_EINVAL;
+    }
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void ensure(size_t count) {
+        if (count <= n && p) return;
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw Error(ORBFE_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        n = count;
+    }
+};
+
+inline int round_even_f(float v) { return (int)std::lrintf(v); }
+inline int floor_f(float v) { int i = (int)v; return i - (i > v); }
+inline int ceil_f(float v) { int i = (int)v; return i + (i < v); }
+inline short sat_short(int v) { return (short)std::min(std::max(v, -32768), 32767); }
+
+}  // namespace
+
+struct orbfe_ctx {
+    orbfe_params prm{};
+    double scale_factor_d = 1.2;
+    std::vector<float> sf, isf, s2, is2;
+    std::vector<int> n_per_level;
+    int umax[16] = {0};
+
+    // geometry of the reserved image size
+    int W = 0, H = 0, max_images = 0;
+    Geo geo{};
+    std::vector<CellGeo> cells;
+    std::vector<ResizeX> xt;
+    std::vector<ResizeY> yt;
+    std::vector<int> chunk_level;
+    int maxcell = 0;
+
+    DevBuf<CellGeo> d_cells;
+    DevBuf<ResizeX> d_xt;
+    DevBuf<ResizeY> d_yt;
+    DevBuf<int> d_chunk_level;
+    DevBuf<uint8_t> d_in;      // staging of the host-buffer API
+    DevBuf<uint8_t> d_ws;
+    DevBuf<int> d_cell_count;
+    DevBuf<uint32_t> d_slots;
+    DevBuf<uint32_t> d_kd;
+    DevBuf<uint16_t> d_kn;
+    DevBuf<uint32_t> d_lvl_kp;
+    DevBuf<int> d_lvl_count;
+    DevBuf<orbfe_keypoint> d_kps;
+    DevBuf<uint8_t> d_desc;
+    DevBuf<int> d_count;
+    DevBuf<int> d_overflow;
+    DevBuf<float> d_uR, d_depth;
+    DevBuf<int8_t> d_status;
+    DevBuf<int32_t> d_match;
+    // hamming scratch
+    DevBuf<uint8_t> d_hq, d_ht;
+    DevBuf<int> d_hoff, d_hidx, d_hres;
+
+    // live profiling: (ORBFE_NSTAGES + 1) events per batch
+    std::vector<hipEvent_t> prof_ev;
+    int prof_max = 0, prof_n = 0;
+    bool prof_on = false;
+
+    hipStream_t own_stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    const uint8_t* last_in = nullptr;  // device input of the last extraction
+    int64_t last_pitch = 0;
+    int last_images = 0, last_pairs = 0;
+    bool have_single = false;          // orbfe_extract ran and its buffers are valid
+
+    ~orbfe_ctx() {
+        for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
+    }
+};
+
+namespace {
+
+// ORBextractor::ORBextractor (ORBextractor.cpp:410-470)
+void build_tables(orbfe_ctx& c) {
+    const orbfe_params& p = c.prm;
+    if (p.nlevels < 1 || p.nlevels > kMaxLevels) throw Error(ORBFE_EINVAL, "nlevels must be in [1, 16]");
+    if (p.nfeatures < 0 || !(p.scale_factor > 0.f)) throw Error(ORBFE_EINVAL, "bad nfeatures / scaleFactor");
+    if (p.resize_simd_lanes != 0 && p.resize_simd_lanes != 16 && p.resize_simd_lanes != 32)
+        throw Error(ORBFE_EINVAL, "resize_simd_lanes must be 0, 16 or 32");
+    const int L = p.nlevels;
+    c.scale_factor_d = (double)p.scale_factor;
+    c.sf.assign(L, 1.0f);
+    c.s2.assign(L, 1.0f);
+    for (int i = 1; i < L; ++i) {
+        c.sf[i] = (float)((double)c.sf[i - 1] * c.scale_factor_d);
+        c.s2[i] = c.sf[i] * c.sf[i];
+    }
+    c.isf.resize(L);
+    c.is2.resize(L);
+    for (int i = 0; i < L; ++i) {
+        c.isf[i] = 1.0f / c.sf[i];
+        c.is2[i] = 1.0f / c.s2[i];
+    }
+    c.n_per_level.assign(L, 0);
+    const float factor = (float)(1.0 / c.scale_factor_d);
+    float want = p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; ++l) {
+        c.n_per_level[l] = round_even_f(want);
+        sum += c.n_per_level[l];
+        want *= factor;
+    }
+    c.n_per_level[L - 1] = std::max(p.nfeatures - sum, 0);
+    const int vmax = floor_f(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+    const int vmin = ceil_f(kHalfPatch * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) c.umax[v] = (int)std::lrint(std::sqrt((double)kHalfPatch * kHalfPatch - v * v));
+    for (int v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+        while (c.umax[v0] == c.umax[v0 + 1]) ++v0;
+        c.umax[v] = v0;
+        ++v0;
+    }
+}
+
+// Resize coefficient tables of cv::resize(INTER_LINEAR) for sw x sh -> dw x dh (8U fixed point).
+void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::vector<ResizeX>& xt,
+                   std::vector<ResizeY>& yt) {
+    const double inv_x = (double)dw / sw, inv_y = (double)dh / sh;
+    const double scale_x = 1. / inv_x, scale_y = 1. / inv_y;
+    const int isx = (int)std::lrint(scale_x), isy = (int)std::lrint(scale_y);
+    const bool area_fast = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON;
+    if (area_fast && isx == 2 && isy == 2)
+        throw Error(ORBFE_EINVAL, "scale factor 2 selects cv::resize's INTER_AREA path, which is not implemented");
+    Lg.xtab_off = (int)xt.size();
+    Lg.ytab_off = (int)yt.size();
+    int xmax = dw;
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = floor_f(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
+        }
+        ResizeX r;
+        r.sx = sx;
+        r.a0 = sat_short(round_even_f((1.f - fx) * 2048));
+        r.a1 = sat_short(round_even_f(fx * 2048));
+        xt.push_back(r);
+    }
+    Lg.xmax = xmax;
+    int xv = 0;
+    if (simd > 0) {
+        while (xv <= dw - simd) xv += simd;
+        while (xv < dw - simd / 2) xv += simd / 2;
+    }
+    Lg.xvec = xv;
+    auto clip = [](int v, int n) { return v >= 0 ? (v < n ? v : n - 1) : 0; };
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = floor_f(fy);
+        fy -= sy;
+        ResizeY r;
+        r.sy0 = clip(sy, sh);
+        r.sy1 = clip(sy + 1, sh);
+        r.b0 = sat_short(round_even_f((1.f - fy) * 2048));
+        r.b1 = sat_short(round_even_f(fy * 2048));
+        yt.push_back(r);
+    }
+}
+
+void build_geometry(orbfe_ctx& c, int W, int H) {
+    const int L = c.prm.nlevels;
+    Geo& g = c.geo;
+    std::memset(&g, 0, sizeof(g));
+    g.nlevels = L;
+    g.W = W;
+    g.H = H;
+    g.ini_th = std::min(std::max(c.prm.ini_th_fast, 0), 255);  // cv::FAST clamps the threshold
+    g.min_th = std::min(std::max(c.prm.min_th_fast, 0), 255);
+    for (int v = 0; v < 16; ++v) g.umax[v] = c.umax[v];
+    c.cells.clear();
+    c.xt.clear();
+    c.yt.clear();
+    c.chunk_level.clear();
+    c.maxcell = 0;
+    int64_t ws = 0;
+    int kp_off = 0, key_off = 0, chunk = 0;
+    int64_t slot_off = 0;
+    for (int l = 0; l < L; ++l) {
+        LevelGeo& Lg = g.lv[l];
+        g.scale[l] = c.sf[l];
+        g.inv_scale[l] = c.isf[l];
+        Lg.scale = c.sf[l];
+        Lg.inv_scale = c.isf[l];
+        Lg.w = round_even_f((float)W * c.isf[l]);
+        Lg.h = round_even_f((float)H * c.isf[l]);
+        if (Lg.w < 1 || Lg.h < 1 || Lg.w > 4095 || Lg.h > 4095)
+            throw Error(ORBFE_EINVAL, "level size out of range (1..4095 px per side)");
+        if (Lg.w <= kEdge || Lg.h <= kEdge)
+            throw Error(ORBFE_EINVAL, "image too small: a pyramid level is not wider than the 19 px reflect border");
+        if (l > 0) {
+            Lg.ws_off = ws;
+            ws += ((int64_t)Lg.w * Lg.h + 255) & ~(int64_t)255;
+            resize_tables(g.lv[l - 1].w, g.lv[l - 1].h, Lg.w, Lg.h, c.prm.resize_simd_lanes, Lg, c.xt, c.yt);
+        }
+        Lg.n_feat = c.n_per_level[l];
+        Lg.size = (float)(int)(31 * c.sf[l]);
+        // cell grid (ORBextractor.cpp:772-806)
+        const int minX = kBorder, minY = kBorder, maxX = Lg.w - kEdge + 3, maxY = Lg.h - kEdge + 3;
+        Lg.span_x = maxX - minX;
+        Lg.span_y = maxY - minY;
+        const float width = (float)(maxX - minX), height = (float)(maxY - minY);
+        const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+        Lg.cell0 = (int)c.cells.size();
+        Lg.key_off = key_off;
+        int key_cap = 0;
+        if (nCols > 0 && nRows > 0) {
+            const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+            for (int i = 0; i < nRows; ++i) {
+                const float iniY = (float)(minY + i * hCell);
+                float maxYc = iniY + hCell + 6;
+                if (iniY >= maxY - 3) continue;
+                if (maxYc > maxY) maxYc = (float)maxY;
+                for (int j = 0; j < nCols; ++j) {
+                    const float iniX = (float)(minX + j * wCell);
+                    float maxXc = iniX + wCell + 6;
+                    if (iniX >= maxX - 6) continue;
+                    if (maxXc > maxX) maxXc = (float)maxX;
+                    CellGeo cg{};
+                    cg.level = (int16_t)l;
+                    cg.x0 = (int16_t)(int)iniX;
+                    cg.y0 = (int16_t)(int)iniY;
+                    cg.x1 = (int16_t)(int)maxXc;
+                    cg.y1 = (int16_t)(int)maxYc;
+                    const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
+                    if (rw > kMaxCellRoi || rh > kMaxCellRoi) throw Error(ORBFE_EINVAL, "FAST cell larger than 64 px");
+                    const int ww = std::max(rw - 6, 0), wh = std::max(rh - 6, 0);
+                    cg.slot_off = (int)slot_off;
+                    cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
+                    slot_off += cg.slot_cap;
+                    key_cap += cg.slot_cap;
+                    c.cells.push_back(cg);
+                }
+            }
+        }
+        Lg.ncell = (int)c.cells.size() - Lg.cell0;
+        Lg.key_cap = key_cap;
+        key_off += key_cap;
+        c.maxcell = std::max(c.maxcell, Lg.ncell);
+        if (key_cap >= (1 << 24)) throw Error(ORBFE_EINVAL, "too many FAST candidates per level");
+        // DistributeOctTree initial columns (:543-545)
+        Lg.n_ini = 0;
+        Lg.hx = 1.f;
+        if (Lg.ncell > 0) {
+            if (Lg.span_y <= 0 || Lg.span_x <= 0) throw Error(ORBFE_EINVAL, "degenerate level");
+            Lg.n_ini = (int)std::round((float)Lg.span_x / Lg.span_y);
+            if (Lg.n_ini <= 0)
+                throw Error(ORBFE_EINVAL, "level aspect ratio < 0.5: the reference octree indexes out of range");
+            Lg.hx = (float)Lg.span_x / Lg.n_ini;
+        }
+        Lg.kp_cap = std::max(Lg.n_feat + 2, 4 * Lg.n_ini) + 2;
+        Lg.kp_off = kp_off;
+        kp_off += Lg.kp_cap;
+        Lg.chunk0 = chunk;
+        const int nch = (Lg.kp_cap + 3) / 4;
+        for (int k = 0; k < nch; ++k) c.chunk_level.push_back(l);
+        chunk += nch;
+        g.max_ncap = std::max(g.max_ncap, Lg.kp_cap);
+    }
+    g.ncells = (int)c.cells.size();
+    g.kp_cap = kp_off;
+    g.lvl_kp_cap = kp_off;
+    g.ws_bytes = std::max<int64_t>(ws, 256);
+    g.slot_total = std::max<int64_t>(slot_off, 1);
+    g.key_total = std::max(key_off, 1);
+    if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
+    if (octree_lds_bytes(g, c.maxcell) > 150 * 1024)
+        throw Error(ORBFE_EINVAL, "octree LDS footprint exceeds the 160 KiB LDS of a CU (nfeatures per level too large)");
+    c.W = W;
+    c.H = H;
+}
+
+void reserve(orbfe_ctx& c, int W, int H, int max_images) {
+    if (W <= 0 || H <= 0 || max_images <= 0) throw Error(ORBFE_EINVAL, "bad reserve geometry");
+    if (W != c.W || H != c.H) {
+        build_geometry(c, W, H);
+        c.max_images = 0;
+        c.d_cells.ensure(c.cells.size());
+        HIPCK(hipMemcpy(c.d_cells.p, c.cells.data(), c.cells.size() * sizeof(CellGeo), hipMemcpyHostToDevice));
+        c.d_xt.ensure(c.xt.size());
+        if (!c.xt.empty())
+            HIPCK(hipMemcpy(c.d_xt.p, c.xt.data(), c.xt.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
+        c.d_yt.ensure(c.yt.size());
+        if (!c.yt.empty())
+            HIPCK(hipMemcpy(c.d_yt.p, c.yt.data(), c.yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+        c.d_chunk_level.ensure(c.chunk_level.size());
+        HIPCK(hipMemcpy(c.d_chunk_level.p, c.chunk_level.data(), c.chunk_level.size() * sizeof(int),
+                        hipMemcpyHostToDevice));
+        c.have_single = false;
+    }
+    if (max_images > c.max_images) {
+        const Geo& g = c.geo;
+        const size_t n = (size_t)max_images;
+        c.d_ws.ensure(n * g.ws_bytes);
+        c.d_cell_count.ensure(n * std::max(g.ncells, 1));
+        c.d_slots.ensure(n * g.slot_total);
+        c.d_kd.ensure(n * g.key_total);
+        c.d_kn.ensure(n * g.key_total);
+        c.d_lvl_kp.ensure(n * g.lvl_kp_cap);
+        c.d_lvl_count.ensure(n * g.nlevels);
+        c.d_kps.ensure(n * g.kp_cap);
+        c.d_desc.ensure(n * g.kp_cap * 32);
+        c.d_count.ensure(n);
+        c.d_overflow.ensure(1);
+        const size_t np = n / 2 + 1;
+        c.d_uR.ensure(np * g.kp_cap);
+        c.d_depth.ensure(np * g.kp_cap);
+        c.d_status.ensure(np * g.kp_cap);
+        c.d_match.ensure(np * g.kp_cap);
+        c.max_images = max_images;
+    }
+}
+
+// record boundary `k` (0..ORBFE_NSTAGES) of the current profiled batch
+void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
+    if (!c.prof_on || c.prof_n >= c.prof_max) return;
+    HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * (ORBFE_NSTAGES + 1) + k], s));
+}
+
+void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hipStream_t s) {
+    const Geo& g = c.geo;
+    if (n <= 0) return;
+    if (n > c.max_images) throw Error(ORBFE_ECAPACITY, "batch larger than the reserved image count");
+    if (pitch < (int64_t)g.W * g.H) throw Error(ORBFE_EINVAL, "image pitch smaller than width*height");
+    HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
+    prof_mark(c, s, 0);
+    for (int l = 1; l < g.nlevels; ++l)
+        HIPCK(launch_resize(g, l, d_in, pitch, c.d_ws.p, c.d_xt.p, c.d_yt.p, n, s));
+    prof_mark(c, s, 1);
+    if (g.ncells > 0)
+        HIPCK(launch_detect(g, c.d_cells.p, d_in, pitch, c.d_ws.p, c.d_cell_count.p, c.d_slots.p, n, s));
+    prof_mark(c, s, 2);
+    HIPCK(launch_octree(g, c.d_cells.p, c.d_cell_count.p, c.d_slots.p, c.d_kd.p, c.d_kn.p, c.d_lvl_kp.p,
+                        c.d_lvl_count.p, c.d_overflow.p, c.maxcell, n, s));
+    prof_mark(c, s, 3);
+    HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p, c.d_count.p,
+                          c.d_chunk_level.p, (int)c.chunk_level.size(), n, s));
+    prof_mark(c, s, 4);
+    c.last_in = d_in;
+    c.last_pitch = pitch;
+    c.last_images = n;
+    c.last_stream = s;
+}
+
+void stereo_consts(double bf, float fx, StereoArgs& a) {
+    const float bf32 = (float)bf;                 // NEP 50: the Python float meets an np.float32
+    const float mb = bf32 / fx;                   // Frame.py:43  mbf / mK[0][0]
+    a.maxD = bf32 / mb;                           // Frame.py:183 mbf / minZ
+    a.bf32 = bf32;
+    a.bf = bf;
+}
+
+void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStream_t s) {
+    const Geo& g = c.geo;
+    if (n_pairs <= 0) return;
+    if (2 * n_pairs > c.last_images) throw Error(ORBFE_ESTATE, "stereo batch needs 2*n_pairs extracted images");
+    StereoArgs a{};
+    a.kpsL = c.d_kps.p;
+    a.kpsR = c.d_kps.p + g.kp_cap;
+    a.kp_stride = 2 * (int64_t)g.kp_cap;
+    a.descL = c.d_desc.p;
+    a.descR = c.d_desc.p + (int64_t)g.kp_cap * 32;
+    a.countL = c.d_count.p;
+    a.countR = c.d_count.p + 1;
+    a.cnt_stride = 2;
+    a.lvl0L = c.last_in;
+    a.lvl0R = c.last_in + c.last_pitch;
+    a.lvl0_stride = 2 * c.last_pitch;
+    a.wsL = c.d_ws.p;
+    a.wsR = c.d_ws.p + g.ws_bytes;
+    a.ws_stride = 2 * g.ws_bytes;
+    a.u_right = c.d_uR.p;
+    a.depth = c.d_depth.p;
+    a.status = c.d_status.p;
+    a.match_r = c.d_match.p;
+    a.out_stride = g.kp_cap;
+    stereo_consts(bf, fx, a);
+    HIPCK(launch_stereo(g, a, n_pairs, s));
+    prof_mark(c, s, 5);
+    if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
+    c.last_pairs = n_pairs;
+}
+
+hipStream_t own(orbfe_ctx& c) {
+    if (!c.own_stream) HIPCK(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
+    return c.own_stream;
+}
+
+void check_overflow(orbfe_ctx& c) {
+    int ovf = 0;
+    HIPCK(hipMemcpy(&ovf, c.d_overflow.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (ovf) throw Error(ORBFE_EOVERFLOW, "on-device capacity bound exceeded (code " + std::to_string(ovf) + ")");
+}
+
+}  // namespace
+
+// ============================================================================================ C ABI
+extern "C" {
+
+const char* orbfe_last_error(void) { return g_err.c_str(); }
+
+const char* orbfe_version(void) { return "orbfe 0.1 gfx950 (HIP, wave64, integer/bitwise, no MFMA)"; }
+
+int orbfe_create(const orbfe_params* params, orbfe_handle* out) {
+    return guarded([&] {
+        if (!params || !out) throw Error(ORBFE_EINVAL, "null argument");
+        std::unique_ptr<orbfe_ctx> c(new orbfe_ctx());
+        c->prm = *params;
+        build_tables(*c);
+        *out = c.release();
+    });
+}
+
+int orbfe_destroy(orbfe_handle h) {
+    return guarded([&] {
+        if (h && h->last_stream) (void)hipStreamSynchronize(h->last_stream);
+        delete h;
+    });
+}
+
+int orbfe_get_scales(orbfe_handle h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                     int32_t* n_per_level) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        for (int l = 0; l < h->prm.nlevels; ++l) {
+            if (scale) scale[l] = h->sf[l];
+            if (inv_scale) inv_scale[l] = h->isf[l];
+            if (sigma2) sigma2[l] = h->s2[l];
+            if (inv_sigma2) inv_sigma2[l] = h->is2[l];
+            if (n_per_level) n_per_level[l] = h->n_per_level[l];
+        }
+    });
+}
+
+int orbfe_batch_reserve(orbfe_handle h, int32_t width, int32_t height, int32_t max_images) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        reserve(*h, width, height, max_images);
+    });
+}
+
+int orbfe_extract(orbfe_handle h, const uint8_t* img, int32_t width, int32_t height, int32_t stride,
+                  orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        *n_out = 0;
+        h->have_single = false;
+        if (width <= 0 || height <= 0) return;  // _image.empty() -> return (ORBextractor.cpp:1045-1046)
+        if (!img || stride < width) throw Error(ORBFE_EINVAL, "bad image pointer / stride");
+        reserve(*h, width, height, std::max(h->max_images, 1));
+        hipStream_t s = own(*h);
+        const size_t bytes = (size_t)width * height;
+        h->d_in.ensure(bytes);
+        HIPCK(hipMemcpy2DAsync(h->d_in.p, width, img, stride, width, height, hipMemcpyHostToDevice, s));
+        enqueue_extract(*h, h->d_in.p, (int64_t)bytes, 1, s);
+        int n = 0;
+        HIPCK(hipMemcpyAsync(&n, h->d_count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        check_overflow(*h);
+        h->have_single = true;
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "keypoint buffer too small");
+        if (n > 0) {
+            if (kps) HIPCK(hipMemcpy(kps, h->d_kps.p, (size_t)n * sizeof(orbfe_keypoint), hipMemcpyDeviceToHost));
+            if (desc) HIPCK(hipMemcpy(desc, h->d_desc.p, (size_t)n * 32, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+int orbfe_pyramid(orbfe_handle h, int32_t level, uint8_t* out, int32_t sheared, int32_t* w_out, int32_t* h_out) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (!h->have_single) throw Error(ORBFE_ESTATE, "no image extracted with orbfe_extract yet");
+        if (level < 0 || level >= h->geo.nlevels) throw Error(ORBFE_EINVAL, "level out of range");
+        const LevelGeo& L = h->geo.lv[level];
+        if (w_out) *w_out = L.w;
+        if (h_out) *h_out = L.h;
+        if (!out) return;
+        std::vector<uint8_t> lv((size_t)L.w * L.h);
+        const uint8_t* src = level == 0 ? h->d_in.p : h->d_ws.p + L.ws_off;
+        HIPCK(hipMemcpy(lv.data(), src, lv.size(), hipMemcpyDeviceToHost));
+        if (!sheared) {
+            std::memcpy(out, lv.data(), lv.size());
+            return;
+        }
+        // ROI data pointer of the 19-px reflect-101 padded level read with stride w (caster ignores step)
+        const int pw = L.w + 2 * kEdge;
+        auto refl = [](int p, int n) {
+            p = p < 0 ? -p : p;
+            return p >= n ? 2 * n - 2 - p : p;
+        };
+        for (int64_t i = 0; i < (int64_t)L.w * L.h; ++i) {
+            const int64_t f = (int64_t)kEdge * pw + kEdge + i;
+            const int pr = (int)(f / pw), pc = (int)(f % pw);
+            out[i] = lv[(size_t)refl(pr - kEdge, L.h) * L.w + refl(pc - kEdge, L.w)];
+        }
+    });
+}
+
+int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, float* u_right, float* depth,
+                       int8_t* status, int32_t* match_r, int32_t n_left) {
+    return guarded([&] {
+        if (!hl || !hr) throw Error(ORBFE_EINVAL, "null handle");
+        if (!hl->have_single || !hr->have_single) throw Error(ORBFE_ESTATE, "both handles must have extracted");
+        if (hl->W != hr->W || hl->H != hr->H || hl->prm.nlevels != hr->prm.nlevels)
+            throw Error(ORBFE_EINVAL, "left/right extractors differ in geometry");
+        const Geo& g = hl->geo;
+        StereoArgs a{};
+        a.kpsL = hl->d_kps.p;
+        a.kpsR = hr->d_kps.p;
+        a.descL = hl->d_desc.p;
+        a.descR = hr->d_desc.p;
+        a.countL = hl->d_count.p;
+        a.countR = hr->d_count.p;
+        a.lvl0L = hl->d_in.p;
+        a.lvl0R = hr->d_in.p;
+        a.wsL = hl->d_ws.p;
+        a.wsR = hr->d_ws.p;
+        a.u_right = hl->d_uR.p;
+        a.depth = hl->d_depth.p;
+        a.status = hl->d_status.p;
+        a.match_r = hl->d_match.p;
+        a.out_stride = g.kp_cap;
+        stereo_consts(bf, fx, a);
+        hipStream_t s = own(*hl);
+        HIPCK(launch_stereo(g, a, 1, s));
+        int nL = 0;
+        HIPCK(hipMemcpyAsync(&nL, hl->d_count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        if (n_left != nL) throw Error(ORBFE_EINVAL, "n_left does not match the left keypoint count");
+        if (nL == 0) return;
+        if (u_right) HIPCK(hipMemcpy(u_right, hl->d_uR.p, nL * sizeof(float), hipMemcpyDeviceToHost));
+        if (depth) HIPCK(hipMemcpy(depth, hl->d_depth.p, nL * sizeof(float), hipMemcpyDeviceToHost));
+        if (status) HIPCK(hipMemcpy(status, hl->d_status.p, nL, hipMemcpyDeviceToHost));
+        if (match_r) HIPCK(hipMemcpy(match_r, hl->d_match.p, nL * sizeof(int32_t), hipMemcpyDeviceToHost));
+    });
+}
+
+int orbfe_extract_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t img_pitch, int32_t n_images,
+                               void* hip_stream) {
+    return guarded([&] {
+        if (!h || !d_images) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
+        h->have_single = false;
+        enqueue_extract(*h, d_images, img_pitch, n_images, (hipStream_t)hip_stream);
+    });
+}
+
+int orbfe_stereo_batch_device(orbfe_handle h, int32_t n_pairs, double bf, float fx, void* hip_stream) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        enqueue_stereo_batch(*h, n_pairs, bf, fx, (hipStream_t)hip_stream);
+    });
+}
+
+int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t img_pitch, int32_t n_pairs,
+                                double bf, float fx, void* hip_stream) {
+    return guarded([&] {
+        if (!h || !d_images) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
+        h->have_single = false;
+        enqueue_extract(*h, d_images, img_pitch, 2 * n_pairs, (hipStream_t)hip_stream);
+        enqueue_stereo_batch(*h, n_pairs, bf, fx, (hipStream_t)hip_stream);
+    });
+}
+
+int orbfe_batch_view_get(orbfe_handle h, orbfe_batch_view* v) {
+    return guarded([&] {
+        if (!h || !v) throw Error(ORBFE_EINVAL, "null argument");
+        v->kp_cap = h->geo.kp_cap;
+        v->n_images = h->last_images;
+        v->n_pairs = h->last_pairs;
+        v->kps = h->d_kps.p;
+        v->desc = h->d_desc.p;
+        v->count = h->d_count.p;
+        v->u_right = h->d_uR.p;
+        v->depth = h->d_depth.p;
+        v->status = h->d_status.p;
+        v->match_r = h->d_match.p;
+        v->overflow = h->d_overflow.p;
+    });
+}
+
+int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (image < 0 || image >= h->last_images) throw Error(ORBFE_EINVAL, "image index out of range");
+        if (h->last_stream) HIPCK(hipStreamSynchronize(h->last_stream));
+        check_overflow(*h);
+        int n = 0;
+        HIPCK(hipMemcpy(&n, h->d_count.p + image, sizeof(int), hipMemcpyDeviceToHost));
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "keypoint buffer too small");
+        const size_t o = (size_t)image * h->geo.kp_cap;
+        if (n && kps) HIPCK(hipMemcpy(kps, h->d_kps.p + o, n * sizeof(orbfe_keypoint), hipMemcpyDeviceToHost));
+        if (n && desc) HIPCK(hipMemcpy(desc, h->d_desc.p + o * 32, (size_t)n * 32, hipMemcpyDeviceToHost));
+    });
+}
+
+int orbfe_batch_fetch_stereo(orbfe_handle h, int32_t pair, float* u_right, float* depth, int8_t* status,
+                             int32_t* match_r, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (pair < 0 || pair >= h->last_pairs) throw Error(ORBFE_EINVAL, "pair index out of range");
+        if (h->last_stream) HIPCK(hipStreamSynchronize(h->last_stream));
+        int n = 0;
+        HIPCK(hipMemcpy(&n, h->d_count.p + 2 * pair, sizeof(int), hipMemcpyDeviceToHost));
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "buffer too small");
+        const size_t o = (size_t)pair * h->geo.kp_cap;
+        if (n && u_right) HIPCK(hipMemcpy(u_right, h->d_uR.p + o, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (n && depth) HIPCK(hipMemcpy(depth, h->d_depth.p + o, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (n && status) HIPCK(hipMemcpy(status, h->d_status.p + o, n, hipMemcpyDeviceToHost));
+        if (n && match_r) HIPCK(hipMemcpy(match_r, h->d_match.p + o, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    });
+}
+
+int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
+                         int32_t* out) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (n_a < 0 || n_b < 0) throw Error(ORBFE_EINVAL, "negative size");
+        if (n_a == 0 || n_b == 0) return;
+        hipStream_t s = own(*h);
+        h->d_hq.ensure((size_t)n_a * 32);
+        h->d_ht.ensure((size_t)n_b * 32);
+        h->d_hres.ensure((size_t)n_a * n_b);
+        HIPCK(hipMemcpyAsync(h->d_hq.p, a_desc, (size_t)n_a * 32, hipMemcpyHostToDevice, s));
+        HIPCK(hipMemcpyAsync(h->d_ht.p, b_desc, (size_t)n_b * 32, hipMemcpyHostToDevice, s));
+        HIPCK(launch_hamming_matrix(h->d_hq.p, n_a, h->d_ht.p, n_b, h->d_hres.p, s));
+        HIPCK(hipMemcpyAsync(out, h->d_hres.p, (size_t)n_a * n_b * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+    });
+}
+
+int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
+                         int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* best_dist,
+                         int32_t* best_idx, int32_t* second_dist, int32_t* second_idx) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (n_query < 0 || n_train < 0) throw Error(ORBFE_EINVAL, "negative size");
+        if (n_query == 0) return;
+        const int ncand = cand_off[n_query];
+        for (int i = 0; i < ncand; ++i)
+            if (cand_idx[i] < 0 || cand_idx[i] >= n_train) throw Error(ORBFE_EINVAL, "candidate index out of range");
+        hipStream_t s = own(*h);
+        h->d_hq.ensure((size_t)n_query * 32);
+        h->d_ht.ensure((size_t)std::max(n_train, 1) * 32);
+        h->d_hoff.ensure((size_t)n_query + 1);
+        h->d_hidx.ensure((size_t)std::max(ncand, 1));
+        h->d_hres.ensure((size_t)4 * n_query + std::max(ncand, 1));
+        HIPCK(hipMemcpyAsync(h->d_hq.p, query_desc, (size_t)n_query * 32, hipMemcpyHostToDevice, s));
+        if (n_train) HIPCK(hipMemcpyAsync(h->d_ht.p, train_desc, (size_t)n_train * 32, hipMemcpyHostToDevice, s));
+        HIPCK(hipMemcpyAsync(h->d_hoff.p, cand_off, ((size_t)n_query + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        if (ncand) HIPCK(hipMemcpyAsync(h->d_hidx.p, cand_idx, (size_t)ncand * sizeof(int), hipMemcpyHostToDevice, s));
+        int* r = h->d_hres.p;
+        HIPCK(launch_hamming_search(h->d_hq.p, n_query, h->d_ht.p, h->d_hoff.p, h->d_hidx.p, r, r + n_query,
+                                    r + 2 * n_query, r + 3 * n_query, nullptr, s));
+        std::vector<int> res((size_t)4 * n_query);
+        HIPCK(hipMemcpyAsync(res.data(), r, res.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        for (int i = 0; i < n_query; ++i) {
+            if (best_dist) best_dist[i] = res[i];
+            if (best_idx) best_idx[i] = res[n_query + i];
+            if (second_dist) second_dist[i] = res[2 * n_query + i];
+            if (second_idx) second_idx[i] = res[3 * n_query + i];
+        }
+    });
+}
+
+int orbfe_profile_begin(orbfe_handle h, int32_t max_batches) {
+    return guarded([&] {
+        if (!h || max_batches < 0) throw Error(ORBFE_EINVAL, "bad argument");
+        const size_t need = (size_t)max_batches * (ORBFE_NSTAGES + 1);
+        while (h->prof_ev.size() < need) {
+            hipEvent_t e;
+            HIPCK(hipEventCreate(&e));
+            h->prof_ev.push_back(e);
+        }
+        h->prof_max = max_batches;
+        h->prof_n = 0;
+        h->prof_on = max_batches > 0;
+    });
+}
+
+int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches) {
+    return guarded([&] {
+        if (!h || !ms_per_stage) throw Error(ORBFE_EINVAL, "null argument");
+        for (int k = 0; k < ORBFE_NSTAGES; ++k) ms_per_stage[k] = 0.f;
+        for (int b = 0; b < h->prof_n; ++b) {
+            hipEvent_t* e = &h->prof_ev[(size_t)b * (ORBFE_NSTAGES + 1)];
+            HIPCK(hipEventSynchronize(e[ORBFE_NSTAGES]));
+            for (int k = 0; k < ORBFE_NSTAGES; ++k) {
+                float ms = 0.f;
+                HIPCK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+                ms_per_stage[k] += ms;
+            }
+        }
+        if (n_batches) *n_batches = h->prof_n;
+        h->prof_on = false;
+    });
+}
+
+int orbfe_debug_candidates(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (!h->have_single) throw Error(ORBFE_ESTATE, "no image extracted with orbfe_extract yet");
+        if (level < 0 || level >= h->geo.nlevels) throw Error(ORBFE_EINVAL, "level out of range");
+        const LevelGeo& L = h->geo.lv[level];
+        std::vector<int> cnt(std::max(L.ncell, 1));
+        std::vector<uint32_t> slots(h->geo.slot_total);
+        if (L.ncell)
+            HIPCK(hipMemcpy(cnt.data(), h->d_cell_count.p + L.cell0, L.ncell * sizeof(int), hipMemcpyDeviceToHost));
+        HIPCK(hipMemcpy(slots.data(), h->d_slots.p, slots.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        int n = 0;
+        for (int i = 0; i < L.ncell; ++i) {
+            const CellGeo& cg = h->cells[L.cell0 + i];
+            for (int j = 0; j < cnt[i]; ++j, ++n) {
+                if (n >= cap) continue;
+                const uint32_t k = slots[cg.slot_off + j];
+                xyr[3 * n] = (int)(k & 0xFFF) - kBorder;
+                xyr[3 * n + 1] = (int)((k >> 12) & 0xFFF) - kBorder;
+                xyr[3 * n + 2] = (int)(k >> 24);
+            }
+        }
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "buffer too small");
+    });
+}
+
+int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (!h->have_single) throw Error(ORBFE_ESTATE, "no image extracted with orbfe_extract yet");
+        if (level < 0 || level >= h->geo.nlevels) throw Error(ORBFE_EINVAL, "level out of range");
+        const LevelGeo& L = h->geo.lv[level];
+        int n = 0;
+        HIPCK(hipMemcpy(&n, h->d_lvl_count.p + level, sizeof(int), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> kp(std::max(n, 1));
+        if (n) HIPCK(hipMemcpy(kp.data(), h->d_lvl_kp.p + L.kp_off, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "buffer too small");
+        for (int i = 0; i < n; ++i) {
+            xyr[3 * i] = (int)(kp[i] & 0xFFF) - kBorder;
+            xyr[3 * i + 1] = (int)((kp[i] >> 12) & 0xFFF) - kBorder;
+            xyr[3 * i + 2] = (int)(kp[i] >> 24);
+        }
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// orbfe_kernels.h — launchers of the gfx950 kernels (orbfe_kernels.hip) used by orbfe_host.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "orbfe_common.h"
+
+namespace orbfe {
+
+// Pointers for k_stereo.  Pair p reads left/right data at base + p * stride, which covers both the
+// interleaved batch layout (images 2p, 2p+1 of one handle) and two single-image handles (stride 0).
+struct StereoArgs {
+    const orbfe_keypoint* kpsL;
+    const orbfe_keypoint* kpsR;
+    int64_t kp_stride;        // keypoints between consecutive pairs (descriptors: kp_stride * 32 bytes)
+    const uint8_t* descL;
+    const uint8_t* descR;
+    const int* countL;
+    const int* countR;
+    int64_t cnt_stride;
+    const uint8_t* lvl0L;     // level 0 = the input images
+    const uint8_t* lvl0R;
+    int64_t lvl0_stride;
+    const uint8_t* wsL;       // levels >= 1
+    const uint8_t* wsR;
+    int64_t ws_stride;
+    float* u_right;
+    float* depth;
+    int8_t* status;
+    int32_t* match_r;
+    int64_t out_stride;
+    float maxD;               // np.float32(bf / np.float32(bf / fx32))   (Frame.py:43, 181-183)
+    float bf32;               // np.float32(bf): what `mbf / disparity` promotes bf to
+    double bf;
+};
+
+hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
+                         const ResizeY* yt, int n_images, hipStream_t s);
+hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
+                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s);
+size_t octree_lds_bytes(const Geo& g, int maxcell);
+hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
+                         uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
+                         hipStream_t s);
+hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
+                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count,
+                           const int* chunk_level, int n_chunks, int n_images, hipStream_t s);
+hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s);
+hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int* out, hipStream_t s);
+hipError_t launch_hamming_search(const uint8_t* q, int nq, const uint8_t* tr, const int* off, const int* idx, int* bd,
+                                 int* bi, int* sd, int* si, int* all_d, hipStream_t s);
+
+}  // namespace orbfe

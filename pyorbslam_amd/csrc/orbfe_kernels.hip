@@ -1,0 +1,1021 @@
+// orbfe_kernels.hip — gfx950 (CDNA4) kernels of the ORB front-end hot path.
+//
+//   k_resize     cv::resize INTER_LINEAR 8U cascade (ComputePyramid, ORBextractor.cpp:1106-1132)
+//   k_detect     per-cell FAST-9/16 + 3x3 NMS + iniTh/minTh fallback + ordered compaction
+//                (ComputeKeyPointsOctTree cell loop, ORBextractor.cpp:768-828)
+//   k_octree     DistributeOctTree (ORBextractor.cpp:539-762), one workgroup per (level, image)
+//   k_describe   IC_Angle + GaussianBlur 7x7 + steered BRIEF, one wavefront per keypoint
+//                (ORBextractor.cpp:77-147, 1074-1103)
+//   k_stereo     Frame.compute_stereo_matches (Frame.py:161-279), one wavefront per left keypoint
+//   k_hamming_*  ORBMatcher.descriptor_distance batched (ORBMatcher.py:12-14)
+//
+// Integer / bitwise work: no MFMA.  Built with -ffp-contract=off; the only fused multiply-adds are the
+// explicit fmaf() of the two descriptor sample coordinates (the reference build contracts exactly
+// those, see oracle/orb_oracle.cpp) and glibc's sinf/cosf polynomials (fma in double).
+#include <hip/hip_runtime.h>
+
+#include "orbfe_common.h"
+#include "orbfe_kernels.h"
+
+namespace orbfe {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "brief_pattern.inc"
+};
+
+// ------------------------------------------------------------------------------- small helpers
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+    // one reflection suffices: every caller overshoots by less than n
+    p = p < 0 ? -p : p;
+    return p >= n ? 2 * n - 2 - p : p;
+}
+
+__device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const uint8_t* in, int64_t in_pitch,
+                                                    const uint8_t* ws, int img, int* stride) {
+    if (l == 0) {
+        *stride = g.W;
+        return in + (int64_t)img * in_pitch;
+    }
+    *stride = g.lv[l].w;
+    return ws + (int64_t)img * g.ws_bytes + g.lv[l].ws_off;
+}
+
+// Block-wide (256 threads) exclusive scan of a[0..n) in LDS, in place; returns the total.
+// Each thread owns a contiguous chunk, so prefixes follow array order.  tmp: 257 ints of LDS.
+__device__ int block_excl_scan(int* a, int n, int* tmp) {
+    const int t = threadIdx.x;
+    const int per = (n + 255) >> 8;
+    const int b = min(t * per, n), e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; ++i) s += a[i];
+    tmp[t] = s;
+    __syncthreads();
+    if (t < 64) {
+        const int v0 = tmp[4 * t], v1 = tmp[4 * t + 1], v2 = tmp[4 * t + 2], v3 = tmp[4 * t + 3];
+        const int tot = v0 + v1 + v2 + v3;
+        int inc = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o, 64);
+            if (t >= o) inc += y;
+        }
+        const int ex = inc - tot;
+        tmp[4 * t] = ex;
+        tmp[4 * t + 1] = ex + v0;
+        tmp[4 * t + 2] = ex + v0 + v1;
+        tmp[4 * t + 3] = ex + v0 + v1 + v2;
+        if (t == 63) tmp[256] = inc;
+    }
+    __syncthreads();
+    int run = tmp[t];
+    for (int i = b; i < e; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    const int total = tmp[256];
+    __syncthreads();
+    return total;
+}
+
+__device__ int block_sum(int v, int* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    int s = 0;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+// ------------------------------------------------------------------------------- k_resize
+// One thread per output pixel of level l (l >= 1), source = unpadded level l-1.
+__global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                                uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
+                                                const ResizeY* __restrict__ yt) {
+    const LevelGeo& L = g.lv[l];
+    const int img = blockIdx.z, dy = blockIdx.y;
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (dx >= L.w) return;
+    int sstride;
+    const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
+    const ResizeY ry = yt[L.ytab_off + dy];
+    const ResizeX rx = xt[L.xtab_off + dx];
+    const uint8_t* r0 = src + (int64_t)ry.sy0 * sstride + rx.sx;
+    const uint8_t* r1 = src + (int64_t)ry.sy1 * sstride + rx.sx;
+    int h0, h1;
+    if (dx < L.xmax) {
+        h0 = r0[0] * rx.a0 + r0[1] * rx.a1;
+        h1 = r1[0] * rx.a0 + r1[1] * rx.a1;
+    } else {
+        h0 = r0[0] * 2048;
+        h1 = r1[0] * 2048;
+    }
+    int v;
+    if (dx < L.xvec) {  // OpenCV VResizeLinearVec_32s8u: v_mul_hi on (S>>4) packed to int16, then (x+2)>>2
+        const int a0 = min(h0 >> 4, 32767), a1 = min(h1 >> 4, 32767);
+        v = (((a0 * ry.b0) >> 16) + ((a1 * ry.b1) >> 16) + 2) >> 2;
+    } else {            // FixedPtCast<int, uchar, 22>
+        v = (h0 * ry.b0 + h1 * ry.b1 + (1 << 21)) >> 22;
+    }
+    ws[(int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy * L.w + dx] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ------------------------------------------------------------------------------- k_detect
+// FAST-9/16 "M" of a pixel: it is a segment-test corner at threshold t iff M > t, and OpenCV's
+// cornerScore is then M - 1.  M = max(v - min_arc max9(I), max_arc min9(I) - v) over the 16 arcs.
+__device__ __forceinline__ int fast_m(const uint8_t* r, int s) {
+    int p[16];
+    p[0] = r[3 * s];
+    p[1] = r[3 * s + 1];
+    p[2] = r[2 * s + 2];
+    p[3] = r[s + 3];
+    p[4] = r[3];
+    p[5] = r[-s + 3];
+    p[6] = r[-2 * s + 2];
+    p[7] = r[-3 * s + 1];
+    p[8] = r[-3 * s];
+    p[9] = r[-3 * s - 1];
+    p[10] = r[-2 * s - 2];
+    p[11] = r[-s - 3];
+    p[12] = r[-3];
+    p[13] = r[s - 3];
+    p[14] = r[2 * s - 2];
+    p[15] = r[3 * s - 1];
+    const int v = r[0];
+    int mx3[16], mn3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mx3[k] = max(max(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
+        mn3[k] = min(min(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
+    }
+    int lo = 255, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        lo = min(lo, max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]));
+        hi = max(hi, min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]));
+    }
+    return max(max(v - lo, hi - v), 0);
+}
+
+// One workgroup per (cell, image).  Output: the cell's keypoints in FAST's row-major order packed as
+// x | y << 12 | score << 24 (level coordinates), and the per-cell count.
+__global__ __launch_bounds__(256) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
+                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
+                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
+    __shared__ uint8_t roi[kMaxCellRoi * kMaxCellRoi];
+    __shared__ uint8_t mm[kMaxCellRoi * kMaxCellRoi];
+    __shared__ int red[8];
+    __shared__ int cnts[256];
+    __shared__ int scan_tmp[257];
+    const int c = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+    const CellGeo cg = cells[c];
+    int stride;
+    const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
+    const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
+    for (int i = t; i < rw * rh; i += 256) {
+        const int y = i / rw, x = i - y * rw;
+        roi[i] = lvl[(int64_t)(cg.y0 + y) * stride + cg.x0 + x];
+    }
+    __syncthreads();
+    const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
+    const int npx = (ww > 0 && wh > 0) ? ww * wh : 0;
+    for (int i = t; i < npx; i += 256) {
+        const int y = i / ww, x = i - y * ww;
+        mm[i] = (uint8_t)fast_m(roi + (y + 3) * rw + x + 3, rw);
+    }
+    __syncthreads();
+    // thread-contiguous chunks in row-major order keep the compaction in FAST's output order
+    const int per = (npx + 255) >> 8;  // <= 14 for a 58x58 window
+    const int b = min(t * per, npx), e = min(b + per, npx);
+    int th = g.ini_th;
+    uint64_t keep_mask = 0;
+    int cnt = 0, total = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        keep_mask = 0;
+        cnt = 0;
+        for (int i = b; i < e; ++i) {
+            const int m = mm[i];
+            if (m <= th) continue;
+            const int s = m - 1;
+            const int y = i / ww, x = i - y * ww;
+            bool keep = true;
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (!dx && !dy) continue;
+                    const int yy = y + dy, xx = x + dx;
+                    int sq = 0;  // outside the window or not a corner at th: score 0
+                    if (yy >= 0 && yy < wh && xx >= 0 && xx < ww) {
+                        const int mq = mm[yy * ww + xx];
+                        sq = mq > th ? mq - 1 : 0;
+                    }
+                    keep = keep && (s > sq);
+                }
+            if (keep) {
+                keep_mask |= 1ull << (i - b);
+                ++cnt;
+            }
+        }
+        total = block_sum(cnt, red);
+        if (total > 0) break;
+        th = g.min_th;  // empty cell at iniThFAST: retry at minThFAST (ORBextractor.cpp:811-815)
+    }
+    cnts[t] = cnt;
+    __syncthreads();
+    block_excl_scan(cnts, 256, scan_tmp);
+    uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
+    int o = cnts[t];
+    for (int i = b; i < e; ++i) {
+        if (!((keep_mask >> (i - b)) & 1ull)) continue;
+        const int y = i / ww, x = i - y * ww;
+        const uint32_t X = (uint32_t)(cg.x0 + x + 3), Y = (uint32_t)(cg.y0 + y + 3), S = (uint32_t)(mm[i] - 1);
+        if (o < cg.slot_cap) out[o] = X | (Y << 12) | (S << 24);  // bound holds by NMS; never write past it
+        ++o;
+    }
+    if (t == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
+}
+
+// ------------------------------------------------------------------------------- k_octree
+// DistributeOctTree as a sequence of data-parallel passes.  The std::list of the reference is held as
+// an array ordered by list position; push_front / erase become "children of this pass at the front in
+// reverse creation order, surviving nodes after them in their old order".  Every candidate key keeps
+// the list position of its node (kn[]), re-mapped after each pass.  Equal-size ties in the careful
+// phase resolve by node creation order (see oracle/orb_oracle.cpp).
+//
+// LDS layout (dynamic, NC = Geo::max_ncap node slots):
+//   box[2][NC] u64 (x0,y0,x1,y1 int16) | cnt[2][NC] i32 | cnt4[4NC] i32 | cpos[4NC] i32 |
+//   sa[NC] sb[NC] sd[NC] proc[NC] i32 | srt[pow2(NC)] u64 | coff[maxcell+1] i32
+struct OctLds {
+    uint64_t *box0, *box1;
+    int *cnt0, *cnt1;
+    int* cnt4;
+    int* cpos;
+    int *sa, *sb, *sd, *proc;
+    uint64_t* srt;
+    int* coff;
+};
+
+__device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
+    const int x = (int)(key & 0xFFFu) - kBorder, y = (int)((key >> 12) & 0xFFFu) - kBorder;
+    const int x0 = (int16_t)(box & 0xFFFF), y0 = (int16_t)((box >> 16) & 0xFFFF);
+    const int x1 = (int16_t)((box >> 32) & 0xFFFF), y1 = (int16_t)((box >> 48) & 0xFFFF);
+    const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);  // ceil((float)d/2), d >= 0
+    return (x < mx ? 0 : 1) + (y < my ? 0 : 2);
+}
+
+__device__ __forceinline__ uint64_t pack_box(int x0, int y0, int x1, int y1) {
+    return (uint64_t)(uint16_t)x0 | ((uint64_t)(uint16_t)y0 << 16) | ((uint64_t)(uint16_t)x1 << 32) |
+           ((uint64_t)(uint16_t)y1 << 48);
+}
+
+// ExtractorNode::DivideNode child boxes (ORBextractor.cpp:483-509), q = 0..3 -> n1..n4
+__device__ __forceinline__ uint64_t child_box(uint64_t box, int q) {
+    const int x0 = (int16_t)(box & 0xFFFF), y0 = (int16_t)((box >> 16) & 0xFFFF);
+    const int x1 = (int16_t)((box >> 32) & 0xFFFF), y1 = (int16_t)((box >> 48) & 0xFFFF);
+    const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+    switch (q) {
+        case 0: return pack_box(x0, y0, mx, my);
+        case 1: return pack_box(mx, y0, x1, my);
+        case 2: return pack_box(x0, my, mx, y1);
+        default: return pack_box(mx, my, x1, y1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict__ cells,
+                                                const int* __restrict__ cell_count, const uint32_t* __restrict__ slots,
+                                                uint32_t* __restrict__ kd_all, uint16_t* __restrict__ kn_all,
+                                                uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
+                                                int* __restrict__ overflow, int maxcell) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int scan_tmp[257];
+    __shared__ int s_S, s_C, s_phase, s_cur, s_nexp, s_P, s_done;
+    const int l = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+    const LevelGeo& L = g.lv[l];
+    const int NC = g.max_ncap;
+    int pow2 = 1;
+    while (pow2 < NC) pow2 <<= 1;
+    OctLds d;
+    {
+        unsigned char* p = lds;
+        d.box0 = (uint64_t*)p; p += 8 * NC;
+        d.box1 = (uint64_t*)p; p += 8 * NC;
+        d.srt = (uint64_t*)p; p += 8 * pow2;
+        d.cnt0 = (int*)p; p += 4 * NC;
+        d.cnt1 = (int*)p; p += 4 * NC;
+        d.cnt4 = (int*)p; p += 16 * NC;
+        d.cpos = (int*)p; p += 16 * NC;
+        d.sa = (int*)p; p += 4 * NC;
+        d.sb = (int*)p; p += 4 * NC;
+        d.sd = (int*)p; p += 4 * NC;
+        d.proc = (int*)p; p += 4 * NC;
+        d.coff = (int*)p;
+    }
+    const int N = L.n_feat;
+    const int ncell = L.ncell;
+    uint32_t* kd = kd_all + (int64_t)img * g.key_total + L.key_off;
+    uint16_t* kn = kn_all + (int64_t)img * g.key_total + L.key_off;
+    uint32_t* out = lvl_kp + (int64_t)img * g.lvl_kp_cap + L.kp_off;
+
+    // 1. gather the level's candidates in cell order (= vToDistributeKeys order)
+    for (int i = t; i < ncell; i += 256) d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+    __syncthreads();
+    const int K = block_excl_scan(d.coff, ncell, scan_tmp);
+    if (t == 0) d.coff[ncell] = K;
+    __syncthreads();
+    const uint32_t* islots = slots + (int64_t)img * g.slot_total;
+    for (int k = t; k < K; k += 256) {
+        int lo = 0, hi = ncell - 1;  // last cell with coff <= k
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        kd[k] = islots[cells[L.cell0 + lo].slot_off + (k - d.coff[lo])];
+    }
+    // 2. initial columns (:543-584); a key goes to column (size_t)(x / hX)
+    const int nIni = L.n_ini;
+    for (int i = t; i < 4 * NC; i += 256) d.cnt4[i] = 0;
+    __syncthreads();
+    for (int k = t; k < K; k += 256) {
+        const int x = (int)(kd[k] & 0xFFFu) - kBorder;
+        int col = (int)((float)x / L.hx);
+        col = min(col, nIni - 1);
+        atomicAdd(&d.cnt4[col], 1);
+        kn[k] = (uint16_t)col;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int S = 0;
+        for (int i = 0; i < nIni; ++i) {
+            const int n = d.cnt4[i];
+            d.cpos[i] = S;
+            if (n > 0) {
+                d.box0[S] = pack_box((int)(L.hx * (float)i), 0, (int)(L.hx * (float)(i + 1)), L.span_y);
+                d.cnt0[S] = n;
+                ++S;
+            }
+        }
+        s_S = S;
+        s_C = 0;
+        s_cur = 0;
+        s_phase = 0;
+        s_done = (S == 0);
+        s_nexp = 0;
+        if (S > NC) { s_done = 1; atomicOr(overflow, 1); }
+    }
+    __syncthreads();
+    for (int k = t; k < K; k += 256) kn[k] = (uint16_t)d.cpos[kn[k]];
+    __syncthreads();
+
+    for (int iter = 0; !s_done; ++iter) {
+        const int S = s_S, C = s_C, cur = s_cur, nxt = cur ^ 1;
+        const uint64_t* box = cur ? d.box1 : d.box0;
+        const int* cnt = cur ? d.cnt1 : d.cnt0;
+        uint64_t* nbox = cur ? d.box0 : d.box1;
+        int* ncnt = cur ? d.cnt0 : d.cnt1;
+        if (iter > 4 * NC + 64) {  // cannot happen (each step grows the list or finishes); never hang
+            if (t == 0) { atomicOr(overflow, 2); s_done = 1; }
+            __syncthreads();
+            break;
+        }
+        if (s_phase == 0) {
+            // ---------------- full pass (:605-664): divide every node holding more than one key
+            for (int i = t; i < 4 * S; i += 256) d.cnt4[i] = 0;
+            if (t == 0) s_nexp = 0;
+            __syncthreads();
+            for (int k = t; k < K; k += 256) {
+                const int p = kn[k];
+                if (cnt[p] > 1) atomicAdd(&d.cnt4[4 * p + quad_of(kd[k], box[p])], 1);
+            }
+            __syncthreads();
+            for (int p = t; p < S; p += 256) {
+                int nc = 0;
+                if (cnt[p] > 1)
+                    for (int q = 0; q < 4; ++q) nc += d.cnt4[4 * p + q] > 0;
+                d.sa[p] = nc;
+                d.sb[p] = cnt[p] == 1;
+            }
+            __syncthreads();
+            const int Cn = block_excl_scan(d.sa, S, scan_tmp);
+            const int Kk = block_excl_scan(d.sb, S, scan_tmp);
+            int nexp = 0;
+            bool ovf = false;
+            for (int p = t; p < S; p += 256) {
+                if (cnt[p] > 1) {
+                    int c = d.sa[p];
+                    for (int q = 0; q < 4; ++q) {
+                        const int n = d.cnt4[4 * p + q];
+                        if (n == 0) continue;
+                        const int np = Cn - 1 - c++;
+                        if (np < NC) {
+                            nbox[np] = child_box(box[p], q);
+                            ncnt[np] = n;
+                        } else {
+                            ovf = true;
+                        }
+                        d.cpos[4 * p + q] = np;
+                        nexp += n > 1;
+                    }
+                } else {
+                    const int np = Cn + d.sb[p];
+                    if (np < NC) {
+                        nbox[np] = box[p];
+                        ncnt[np] = cnt[p];
+                    } else {
+                        ovf = true;
+                    }
+                    d.cpos[4 * p] = np;
+                }
+            }
+            if (nexp) atomicAdd(&s_nexp, nexp);
+            if (ovf) atomicOr(overflow, 4);
+            __syncthreads();
+            for (int k = t; k < K; k += 256) {
+                const int p = kn[k];
+                kn[k] = (uint16_t)(cnt[p] > 1 ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p]);
+            }
+            __syncthreads();
+            if (t == 0) {
+                const int Sn = Cn + Kk;
+                s_S = Sn;
+                s_C = Cn;
+                s_cur = nxt;
+                if (Sn > NC) s_done = 1;
+                else if (Sn >= N || Sn == S) s_done = 1;            // :668-671
+                else if (Sn + 3 * s_nexp > N) s_phase = 1;          // :672
+            }
+            __syncthreads();
+        } else {
+            // ---------------- careful phase (:675-736): divide the largest nodes of the last step first
+            for (int i = t; i < 4 * C; i += 256) d.cnt4[i] = 0;
+            for (int p = t; p < S; p += 256) d.proc[p] = 0;
+            if (t == 0) s_P = 0x7fffffff;
+            __syncthreads();
+            for (int k = t; k < K; k += 256) {
+                const int p = kn[k];
+                if (p < C && cnt[p] > 1) atomicAdd(&d.cnt4[4 * p + quad_of(kd[k], box[p])], 1);
+            }
+            for (int p = t; p < C; p += 256) d.sa[p] = cnt[p] > 1;
+            __syncthreads();
+            const int M = block_excl_scan(d.sa, C, scan_tmp);
+            int m2 = 1;
+            while (m2 < M) m2 <<= 1;
+            for (int p = t; p < C; p += 256)
+                if (cnt[p] > 1)  // size desc, then creation desc (= list position asc)
+                    d.srt[d.sa[p]] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
+            for (int j = M + t; j < m2; j += 256) d.srt[j] = 0;
+            __syncthreads();
+            for (int k2 = 2; k2 <= m2; k2 <<= 1) {  // bitonic sort, descending
+                for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+                    for (int i = t; i < m2; i += 256) {
+                        const int ixj = i ^ j2;
+                        if (ixj > i) {
+                            const uint64_t a = d.srt[i], bb = d.srt[ixj];
+                            const bool desc = (i & k2) == 0;
+                            if (desc ? (a < bb) : (a > bb)) {
+                                d.srt[i] = bb;
+                                d.srt[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // sorted candidate j -> position p, children count, running list size
+            for (int j = t; j < M; j += 256) {
+                const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
+                int nc = 0;
+                for (int q = 0; q < 4; ++q) nc += d.cnt4[4 * p + q] > 0;
+                d.sb[j] = nc - 1;
+                d.sd[j] = nc;
+            }
+            __syncthreads();
+            block_excl_scan(d.sb, M, scan_tmp);
+            for (int j = t; j < M; j += 256)
+                if (S + d.sb[j] + d.sd[j] - 1 >= N) atomicMin(&s_P, j);  // :729-730 break
+            __syncthreads();
+            const int P = s_P == 0x7fffffff ? M : s_P + 1;
+            for (int j = t; j < M; j += 256) {
+                if (j >= P) d.sd[j] = 0;
+                else {
+                    const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
+                    d.proc[p] = 1;
+                }
+            }
+            __syncthreads();
+            const int Cn = block_excl_scan(d.sd, M, scan_tmp);
+            for (int p = t; p < S; p += 256) d.sa[p] = d.proc[p] == 0;
+            __syncthreads();
+            const int Kk = block_excl_scan(d.sa, S, scan_tmp);
+            bool ovf = false;
+            for (int j = t; j < P; j += 256) {
+                const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
+                int c = d.sd[j];
+                for (int q = 0; q < 4; ++q) {
+                    const int n = d.cnt4[4 * p + q];
+                    if (n == 0) continue;
+                    const int np = Cn - 1 - c++;
+                    if (np < NC) {
+                        nbox[np] = child_box(box[p], q);
+                        ncnt[np] = n;
+                    } else {
+                        ovf = true;
+                    }
+                    d.cpos[4 * p + q] = np;
+                }
+            }
+            for (int p = t; p < S; p += 256) {
+                if (d.proc[p]) continue;
+                const int np = Cn + d.sa[p];
+                if (np < NC) {
+                    nbox[np] = box[p];
+                    ncnt[np] = cnt[p];
+                } else {
+                    ovf = true;
+                }
+                d.cpos[4 * p] = np;
+            }
+            if (ovf) atomicOr(overflow, 8);
+            __syncthreads();
+            for (int k = t; k < K; k += 256) {
+                const int p = kn[k];
+                kn[k] = (uint16_t)(d.proc[p] ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p]);
+            }
+            __syncthreads();
+            if (t == 0) {
+                const int Sn = Cn + Kk;
+                s_S = Sn;
+                s_C = Cn;
+                s_cur = nxt;
+                if (Sn > NC || Sn >= N || Sn == S) s_done = 1;  // :733-734
+            }
+            __syncthreads();
+        }
+    }
+    // 3. keep the first maximum-response key of every node (:740-759), list order
+    const int S = min(s_S, NC);
+    uint32_t* best = (uint32_t*)d.cnt4;
+    for (int p = t; p < S; p += 256) best[p] = 0;
+    __syncthreads();
+    for (int k = t; k < K; k += 256) {
+        const int p = kn[k];
+        if (p < S) atomicMax(&best[p], (kd[k] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
+    }
+    __syncthreads();
+    for (int p = t; p < S; p += 256) {
+        const uint32_t k = 0xFFFFFFu - (best[p] & 0xFFFFFFu);
+        if (best[p] != 0u && (int)k < K) {
+            out[p] = kd[k];
+        } else {  // a node without keys cannot occur; flag instead of reading out of range
+            out[p] = 0u;
+            atomicOr(overflow, 16);
+        }
+    }
+    if (t == 0) lvl_count[img * g.nlevels + l] = S;
+}
+
+// ------------------------------------------------------------------------------- k_describe
+// glibc 2.35 x86-64 sinf / cosf (FMA ifunc variant; ARM optimized-routines algorithm), |x| < 120.
+struct SinCosTab {
+    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
+};
+__constant__ SinCosTab c_sc[2] = {
+    {{1, -1, -1, 1}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p+0, -0x1.ffffffd0c621cp-2,
+     -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
+     -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {{1, -1, -1, 1}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p+0, 0x1.ffffffd0c621cp-2,
+     -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
+     -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
+
+__device__ __forceinline__ float sc_sin_poly(double x, double x2, const SinCosTab& p) {
+    const double x3 = x * x2, s1 = __fma_rn(x2, p.s3, p.s2), x5 = x2 * x3, s = __fma_rn(x3, p.s1, x);
+    return (float)__fma_rn(x5, s1, s);
+}
+__device__ __forceinline__ float sc_cos_poly(double x2, const SinCosTab& p) {
+    const double x4 = x2 * x2, c1 = __fma_rn(x2, p.c1, p.c0), c2 = __fma_rn(x2, p.c4, p.c3), x6 = x2 * x4;
+    const double c = __fma_rn(x4, p.c2, c1);
+    return (float)__fma_rn(x6, c2, c);
+}
+__device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
+    const unsigned top = (__float_as_uint(y) >> 20) & 0x7ff;
+    double x = y;
+    if (top <= 0x3f3) {
+        const double x2 = x * x;
+        *sn = top <= 0x397 ? y : sc_sin_poly(x, x2, c_sc[0]);
+        *cs = top <= 0x397 ? 1.0f : sc_cos_poly(x2, c_sc[0]);
+        return;
+    }
+    const double r = x * c_sc[0].hpi_inv;
+    const int n = (((int)r) + 0x800000) >> 24;
+    x = __fma_rn(-(double)n, c_sc[0].hpi, x);
+    const SinCosTab& p = c_sc[(n >> 1) & 1];
+    const double x2 = x * x;
+    const double xs = x * c_sc[0].sign[n & 3];
+    if (n & 1) {
+        *sn = sc_cos_poly(x2, p);
+        *cs = sc_sin_poly(xs, x2, p);
+    } else {
+        *sn = sc_sin_poly(xs, x2, p);
+        *cs = sc_cos_poly(x2, p);
+    }
+}
+
+// cv::fastAtan2, plain IEEE float ops (no contraction)
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (ax >= ay) {
+        const float c = __fdiv_rn(ay, __fadd_rn(ax, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
+        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    } else {
+        const float c = __fdiv_rn(ax, __fadd_rn(ay, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
+        a = __fsub_rn(90.f,
+                      __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+    }
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+constexpr int kDescWaves = 4;
+constexpr int kHbStride = kBlurD;  // horizontal-pass rows of 37 columns
+
+// One wavefront per keypoint.  The 43x43 neighbourhood (reflect-101 at the level border, which is
+// where cv::GaussianBlur on the level clone reflects) is staged in LDS once and serves the intensity
+// centroid (radius 15, never reflected), the separable 7x7 blur of the 37x37 sampling disc and the
+// 256 rotated comparisons (assembled by __ballot, 64 bits per round).
+__global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                                  const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
+                                                  const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
+                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
+                                                  const int* __restrict__ chunk_level) {
+    __shared__ uint8_t patch[kDescWaves][kPatchD * kPatchD];
+    __shared__ uint16_t hb[kDescWaves][kPatchD * kHbStride];
+    __shared__ uint8_t blur[kDescWaves][kBlurD * kBlurD];
+    const int img = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int l = chunk_level[blockIdx.x];
+    const LevelGeo& L = g.lv[l];
+    const int idx = (blockIdx.x - L.chunk0) * kDescWaves + w;
+    const int* cnt = lvl_count + img * g.nlevels;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int s = 0;
+        for (int i = 0; i < g.nlevels; ++i) s += cnt[i];
+        out_count[img] = s;
+    }
+    const bool active = idx < cnt[l];
+    int stride;
+    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
+    int cx = 0, cy = 0, score = 0;
+    if (active) {
+        const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
+        cx = key & 0xFFF;
+        cy = (key >> 12) & 0xFFF;
+        score = key >> 24;
+        for (int i = lane; i < kPatchD * kPatchD; i += 64) {
+            const int r = i / kPatchD - kPatchR, c = i % kPatchD - kPatchR;
+            patch[w][i] = lvl[(int64_t)reflect101(cy + r, L.h) * stride + reflect101(cx + c, L.w)];
+        }
+    }
+    __syncthreads();
+    float angle = 0.f;
+    if (active) {
+        // intensity centroid over the umax disc (IC_Angle, :77-104): m10 = sum u*I, m01 = sum v*I
+        int m10 = 0, m01 = 0;
+        for (int i = lane; i < 31 * 31; i += 64) {
+            const int v = i / 31 - kHalfPatch, u = i % 31 - kHalfPatch;
+            const int av = v < 0 ? -v : v;
+            if ((u < 0 ? -u : u) <= g.umax[av]) {
+                const int val = patch[w][(kPatchR + v) * kPatchD + kPatchR + u];
+                m10 += u * val;
+                m01 += v * val;
+            }
+        }
+        m10 = wave_sum(m10);
+        m01 = wave_sum(m01);
+        angle = fast_atan2((float)m01, (float)m10);
+        // horizontal 7-tap pass over 43 rows x 37 columns
+        for (int i = lane; i < kPatchD * kBlurD; i += 64) {
+            const int r = i / kBlurD, c = i % kBlurD;
+            const uint8_t* s = &patch[w][r * kPatchD + c];
+            hb[w][i] = (uint16_t)(18 * s[0] + 34 * s[1] + 48 * s[2] + 56 * s[3] + 48 * s[4] + 34 * s[5] + 18 * s[6]);
+        }
+    }
+    __syncthreads();
+    if (active) {
+        for (int i = lane; i < kBlurD * kBlurD; i += 64) {
+            const int r = i / kBlurD, c = i % kBlurD;
+            const uint16_t* s = &hb[w][r * kBlurD + c];
+            const int v = 18 * s[0] + 34 * s[kBlurD] + 48 * s[2 * kBlurD] + 56 * s[3 * kBlurD] + 48 * s[4 * kBlurD] +
+                          34 * s[5 * kBlurD] + 18 * s[6 * kBlurD];
+            blur[w][i] = (uint8_t)((v + 32768) >> 16);
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const float factorPI = (float)(M_PI / 180.f);
+    float b, a;
+    glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
+    int o = idx;
+    for (int i = 0; i < l; ++i) o += cnt[i];
+    uint64_t* dst = (uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32);
+#pragma unroll
+    for (int rnd = 0; rnd < 4; ++rnd) {
+        const int bit = rnd * 64 + lane;
+        int val[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float px = (float)c_pattern[4 * bit + 2 * k], py = (float)c_pattern[4 * bit + 2 * k + 1];
+            const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
+            const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
+            val[k] = blur[w][(kBlurR + rr) * kBlurD + kBlurR + cc];
+        }
+        const uint64_t m = __ballot(val[0] < val[1]);
+        if (lane == 0) dst[rnd] = m;
+    }
+    if (lane == 0) {
+        orbfe_keypoint kp;
+        kp.x = l ? __fmul_rn((float)cx, L.scale) : (float)cx;
+        kp.y = l ? __fmul_rn((float)cy, L.scale) : (float)cy;
+        kp.size = L.size;
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        out_kp[(int64_t)img * g.kp_cap + o] = kp;
+    }
+}
+
+// ------------------------------------------------------------------------------- k_stereo
+__device__ __forceinline__ int sheared_px(const uint8_t* lvl, int stride, int w, int h, int r, int c) {
+    // GetImagePyramid's caster reads the padded level's ROI pointer with a contiguous stride of w
+    const int pw = w + 2 * kEdge;
+    const int f = kEdge * pw + kEdge + r * w + c;
+    const int pr = f / pw, pc = f - pr * pw;
+    return lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)];
+}
+
+__device__ __forceinline__ double py_round(double v) { return rint(v); }  // Python round(): half to even
+
+__global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
+    __shared__ int sad[4][11];
+    const int pr = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int iL = blockIdx.x * 4 + w;
+    const int nL = A.countL[pr * A.cnt_stride], nR = A.countR[pr * A.cnt_stride];
+    const bool active = iL < nL;
+    const orbfe_keypoint* KL = A.kpsL + pr * A.kp_stride;
+    const orbfe_keypoint* KR = A.kpsR + pr * A.kp_stride;
+    const uint8_t* DL = A.descL + pr * A.kp_stride * 32;
+    const uint8_t* DR = A.descR + pr * A.kp_stride * 32;
+    if (lane < 11) sad[w][lane] = 0;
+    int best = 256, bidx = 0x7fffffff;
+    orbfe_keypoint kl;
+    if (active) {
+        kl = KL[iL];
+        const int row = (int)(double)kl.y;
+        const float minU = __fsub_rn(kl.x, A.maxD);
+        const uint4* dl4 = (const uint4*)(DL + (int64_t)iL * 32);
+        const uint4 a0 = dl4[0], a1 = dl4[1];
+        for (int c0 = 0; c0 < nR; c0 += 64) {
+            const int iR = c0 + lane;
+            if (iR >= nR) break;
+            const orbfe_keypoint kr = KR[iR];
+            const double r = 2.0 * (double)g.scale[kr.octave];
+            const double maxr = ceil((double)kr.y + r), minr = floor((double)kr.y - r);
+            if (!(minr <= row && row <= maxr)) continue;
+            if (kr.octave < kl.octave - 1 || kr.octave > kl.octave + 1) continue;
+            if (!(minU <= kr.x && (double)kr.x <= (double)kl.x)) continue;
+            const uint4* dr4 = (const uint4*)(DR + (int64_t)iR * 32);
+            const uint4 b0 = dr4[0], b1 = dr4[1];
+            const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                             __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+            if (dist < best) {  // per-lane first minimum (lane's iR increase)
+                best = dist;
+                bidx = iR;
+            }
+        }
+    }
+    // wave argmin on (dist, iR): the reference keeps the first strict minimum in ascending iR
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bidx, o, 64);
+        if (ob < best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+    }
+    __syncthreads();
+    int status = 0;
+    float uR = -1.f, depth = -1.f;
+    const bool refine = active && best < 100 && best < 75;  // TH_HIGH start, thOrbDist = 75 (:166, :203, :222)
+    int scaleduR0 = 0, scaledvL = 0, scaleduL = 0, lw = 0, lh = 0, lstride = 0, rstride = 0;
+    const uint8_t *lvlL = nullptr, *lvlR = nullptr;
+    bool do_sad = false;
+    if (refine) {
+        const int oct = kl.octave;
+        const double isf = (double)g.inv_scale[oct];
+        const float uR0 = KR[bidx].x;
+        scaleduL = (int)py_round((double)kl.x * isf);
+        scaledvL = (int)py_round((double)kl.y * isf);
+        scaleduR0 = (int)py_round((double)uR0 * isf);
+        lw = g.lv[oct].w;
+        lh = g.lv[oct].h;
+        if (oct == 0) {
+            lvlL = A.lvl0L + pr * A.lvl0_stride;
+            lvlR = A.lvl0R + pr * A.lvl0_stride;
+            lstride = rstride = g.W;
+        } else {
+            lvlL = A.wsL + pr * A.ws_stride + g.lv[oct].ws_off;
+            lvlR = A.wsR + pr * A.ws_stride + g.lv[oct].ws_off;
+            lstride = rstride = lw;
+        }
+        // iniu < 0 or endu >= cols (:240-243); slices stay inside the level otherwise
+        do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
+                 scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
+    }
+    if (do_sad) {
+        const int lc = sheared_px(lvlL, lstride, lw, lh, scaledvL, scaleduL);
+        // 11 shifts x 11 rows = 121 row sums of 11 |(IL - IL[5,5]) - (IR - IR[5,5])| terms
+        for (int it = lane; it < 121; it += 64) {
+            const int s = it / 11, r = it % 11, inc = s - 5;
+            const int yy = scaledvL - 5 + r;
+            const int rc = sheared_px(lvlR, rstride, lw, lh, scaledvL, scaleduR0 + inc);
+            int acc = 0;
+            for (int c = 0; c < 11; ++c) {
+                const int il = sheared_px(lvlL, lstride, lw, lh, yy, scaleduL - 5 + c) - lc;
+                const int ir = sheared_px(lvlR, rstride, lw, lh, yy, scaleduR0 + inc - 5 + c) - rc;
+                const int dd = il - ir;
+                acc += dd < 0 ? -dd : dd;
+            }
+            atomicAdd(&sad[w][s], acc);
+        }
+    }
+    __syncthreads();
+    if (do_sad && lane == 0) {
+        int bi = 0, bd = sad[w][0];
+        for (int s = 1; s < 11; ++s)
+            if (sad[w][s] < bd) {
+                bd = sad[w][s];
+                bi = s;
+            }
+        if (bi != 0 && bi != 10) {
+            const int d1 = sad[w][bi - 1], d2 = sad[w][bi], d3 = sad[w][bi + 1];
+            const float deltaR = __fdiv_rn((float)(d1 - d3), (float)(2 * (d1 + d3 - 2 * d2)));
+            if (!(deltaR < -1.f || deltaR > 1.f)) {
+                const float bestuR = __fmul_rn(g.scale[kl.octave], __fadd_rn((float)(scaleduR0 + bi - 5), deltaR));
+                const float disparity = __fsub_rn(kl.x, bestuR);
+                if (0.f <= disparity && disparity < A.maxD) {
+                    if (disparity <= 0.f) {  // Python-double substitution, recomputed on the host
+                        status = 2;
+                        uR = (float)((double)kl.x - 0.01);
+                        depth = (float)(A.bf / 0.01);
+                    } else {
+                        status = 1;
+                        uR = bestuR;
+                        depth = __fdiv_rn(A.bf32, disparity);
+                    }
+                }
+            }
+        }
+    }
+    if (active && lane == 0) {
+        const int64_t o = pr * A.out_stride + iL;
+        A.u_right[o] = status ? uR : -1.f;
+        A.depth[o] = status ? depth : -1.f;
+        A.status[o] = (int8_t)status;
+        A.match_r[o] = status ? bidx : -1;
+    }
+}
+
+// ------------------------------------------------------------------------------- Hamming
+// All-pairs distances: one thread per (a, b) pair, descriptors as 2 x uint4.
+__global__ __launch_bounds__(256) void k_hamming_matrix(const uint8_t* __restrict__ a, int na, const uint8_t* __restrict__ b,
+                                                        int nb, int* __restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y;
+    if (j >= nb) return;
+    const uint4* A4 = (const uint4*)(a + (int64_t)i * 32);
+    const uint4* B4 = (const uint4*)(b + (int64_t)j * 32);
+    const uint4 a0 = A4[0], a1 = A4[1], b0 = B4[0], b1 = B4[1];
+    out[(int64_t)i * nb + j] = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                               __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Candidate-list search: one wavefront per query; keeps the two smallest (dist, position) pairs in
+// lexicographic order, which is what the sequential `dist < best ... elif dist < best2` scan of
+// search_by_projection_f_p (ORBMatcher.py:258-274) leaves in best / best2.  Also writes every
+// candidate distance (CSR order) for host-side control logic that depends on earlier matches.
+__global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ tr,
+                                                        const int* __restrict__ off, const int* __restrict__ idx,
+                                                        int* __restrict__ best_d, int* __restrict__ best_i,
+                                                        int* __restrict__ sec_d, int* __restrict__ sec_i,
+                                                        int* __restrict__ all_d) {
+    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (qi >= nq) return;
+    const uint4* Q4 = (const uint4*)(q + (int64_t)qi * 32);
+    const uint4 a0 = Q4[0], a1 = Q4[1];
+    const int b = off[qi], e = off[qi + 1];
+    int d1 = 256, p1 = 0x7fffffff, d2 = 256, p2 = 0x7fffffff;
+    for (int pos = b + lane; pos < e; pos += 64) {
+        const uint4* T4 = (const uint4*)(tr + (int64_t)idx[pos] * 32);
+        const uint4 b0 = T4[0], b1 = T4[1];
+        const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                      __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+        if (all_d) all_d[pos] = d;
+        if (d < d1) {
+            d2 = d1; p2 = p1; d1 = d; p1 = pos;
+        } else if (d < d2) {
+            d2 = d; p2 = pos;
+        }
+    }
+    // merge top-2 lists across the wave (lexicographic (dist, pos))
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int od1 = __shfl_xor(d1, o, 64), op1 = __shfl_xor(p1, o, 64);
+        const int od2 = __shfl_xor(d2, o, 64), op2 = __shfl_xor(p2, o, 64);
+        int cd[4] = {d1, d2, od1, od2}, cp[4] = {p1, p2, op1, op2};
+        int bd1 = 257, bp1 = 0x7fffffff, bd2 = 257, bp2 = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool lt1 = cd[k] < bd1 || (cd[k] == bd1 && cp[k] < bp1);
+            const bool lt2 = cd[k] < bd2 || (cd[k] == bd2 && cp[k] < bp2);
+            if (lt1) { bd2 = bd1; bp2 = bp1; bd1 = cd[k]; bp1 = cp[k]; }
+            else if (lt2) { bd2 = cd[k]; bp2 = cp[k]; }
+        }
+        d1 = bd1; p1 = bp1; d2 = bd2; p2 = bp2;
+    }
+    if (lane == 0) {
+        best_d[qi] = p1 == 0x7fffffff ? 256 : d1;
+        best_i[qi] = p1 == 0x7fffffff ? -1 : idx[p1];
+        sec_d[qi] = p2 == 0x7fffffff ? 256 : d2;
+        sec_i[qi] = p2 == 0x7fffffff ? -1 : idx[p2];
+    }
+}
+
+// ------------------------------------------------------------------------------- launchers
+hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
+                         const ResizeY* yt, int n_images, hipStream_t s) {
+    dim3 grid((g.lv[l].w + 255) / 256, g.lv[l].h, n_images);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, g, l, in, in_pitch, ws, xt, yt);
+    return hipGetLastError();
+}
+
+hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
+                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s) {
+    hipLaunchKernelGGL(k_detect, dim3(g.ncells, n_images), dim3(256), 0, s, g, cells, in, in_pitch, ws, cell_count,
+                       slots);
+    return hipGetLastError();
+}
+
+size_t octree_lds_bytes(const Geo& g, int maxcell) {
+    const int NC = g.max_ncap;
+    int pow2 = 1;
+    while (pow2 < NC) pow2 <<= 1;
+    return (size_t)8 * NC * 2 + 8 * pow2 + 4 * NC * 2 + 16 * NC * 2 + 4 * NC * 4 + 4 * (maxcell + 1);
+}
+
+hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
+                         uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
+                         hipStream_t s) {
+    const size_t lds = octree_lds_bytes(g, maxcell);
+    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, n_images), dim3(256), lds, s, g, cells, cell_count, slots, kd, kn,
+                       lvl_kp, lvl_count, overflow, maxcell);
+    return hipGetLastError();
+}
+
+hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
+                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count,
+                           const int* chunk_level, int n_chunks, int n_images, hipStream_t s) {
+    hipLaunchKernelGGL(k_describe, dim3(n_chunks, n_images), dim3(256), 0, s, g, in, in_pitch, ws, lvl_kp, lvl_count,
+                       out_kp, out_desc, out_count, chunk_level);
+    return hipGetLastError();
+}
+
+hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
+    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 3) / 4, n_pairs), dim3(256), 0, s, g, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int* out, hipStream_t s) {
+    if (na == 0 || nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hamming_matrix, dim3((nb + 255) / 256, na), dim3(256), 0, s, a, na, b, nb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_hamming_search(const uint8_t* q, int nq, const uint8_t* tr, const int* off, const int* idx, int* bd,
+                                 int* bi, int* sd, int* si, int* all_d, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hamming_search, dim3((nq + 3) / 4), dim3(256), 0, s, q, nq, tr, off, idx, bd, bi, sd, si, all_d);
+    return hipGetLastError();
+}
+
+}  // namespace orbfe

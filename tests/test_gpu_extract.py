@@ -1,0 +1,141 @@
+"""GPU parity of the extractor, stage by stage, against the CPU oracle (bit-exact: integer pixels,
+integer keypoint coordinates / scores, float32 keypoint fields compared bitwise, descriptor bytes)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import KITTI, EUROC
+from oracle import oracle as O
+from pyorbslam_amd import synth
+from pyorbslam_amd._lib import call, ptr
+from pyorbslam_amd.pyORBExtractor import ORBextractor
+
+pytestmark = pytest.mark.gpu
+
+
+def _images(kitti_png):
+    L0, R0 = synth.make_pair(0)
+    Le, _ = synth.make_pair(100, 752, 480)
+    rng = np.random.default_rng(5)
+    noise = rng.integers(0, 256, (376, 1241)).astype(np.uint8)
+    small = synth.make_pair(9, 211, 157)[0]
+    odd = synth.make_pair(11, 641, 333)[1]
+    return {"kitti_L": (L0, KITTI), "kitti_R": (R0, KITTI), "kitti06": (kitti_png, KITTI), "euroc": (Le, EUROC),
+            "noise": (noise, KITTI), "small": (small, dict(KITTI, nfeatures=500)), "odd": (odd, KITTI)}
+
+
+def _debug(ex, fn, level, cap=400000):
+    buf = np.zeros((cap, 3), np.int32)
+    n = C.c_int32()
+    call(fn, ex.handle, level, ptr(buf), cap, C.byref(n))
+    return buf[:n.value].copy()
+
+
+def _first_diff(a, b):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i].tobytes() != b[i].tobytes():
+            return i, a[i], b[i]
+    return n, None, None
+
+
+@pytest.fixture(scope="module")
+def cases(kitti_png):
+    out = {}
+    for name, (img, params) in _images(kitti_png).items():
+        ex = ORBextractor(**params)
+        kps, desc = ex.extract(img)
+        orc = O.OracleExtractor(**params)
+        okps, odesc = orc.extract(img)
+        out[name] = (img, params, ex, kps.copy(), desc.copy(), orc, okps, odesc)
+    return out
+
+
+@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+def test_pyramid(cases, name):
+    img, params, ex, *_rest = cases[name]
+    orc = cases[name][5]
+    for l, (g, o) in enumerate(zip(ex.GetImagePyramid(sheared=False), orc.pyramid())):
+        assert g.shape == o.shape and np.array_equal(g, o), f"level {l}"
+    for l, (g, o) in enumerate(zip(ex.GetImagePyramid(), orc.sheared_pyramid())):
+        assert np.array_equal(g, o), f"sheared level {l}"
+
+
+@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+def test_fast_cells(cases, name):
+    img, params, ex, kps, desc, orc, okps, odesc = cases[name]
+    p = O.Params(params["nfeatures"], params["scaleFactor"], params["nlevels"], params["iniThFAST"],
+                 params["minThFAST"], 16)
+    for l, lvl in enumerate(orc.pyramid()):
+        got = _debug(ex, "orbfe_debug_candidates", l)
+        exp = O.level_candidates(p, lvl)
+        assert len(got) == len(exp), f"level {l}: {len(got)} vs {len(exp)}"
+        i, a, b = _first_diff(got, exp)
+        assert a is None, f"level {l} first diff at {i}: {a} vs {b}"
+
+
+@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+def test_octree(cases, name):
+    img, params, ex, kps, desc, orc, okps, odesc = cases[name]
+    npl = ex.features_per_level()
+    for l, lvl in enumerate(orc.pyramid()):
+        h, w = lvl.shape
+        cand = _debug(ex, "orbfe_debug_candidates", l)
+        got = _debug(ex, "orbfe_debug_selected", l)
+        exp = O.octree(cand, 16, w - 16, 16, h - 16, npl[l])
+        assert len(got) == len(exp), f"level {l}: {len(got)} vs {len(exp)}"
+        i, a, b = _first_diff(got, exp)
+        assert a is None, f"level {l} first diff at {i}: {a} vs {b}"
+
+
+@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+def test_keypoints_and_descriptors_bit_exact(cases, name):
+    img, params, ex, kps, desc, orc, okps, odesc = cases[name]
+    assert len(kps) == len(okps)
+    for f in ("x", "y", "size", "angle", "response", "octave"):
+        i, a, b = _first_diff(kps[f], okps[f])
+        assert a is None, f"field {f} differs at {i}: {a} vs {b}"
+    assert desc.shape == odesc.shape
+    bad = np.nonzero((desc != odesc).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} descriptors differ, first at {bad[:5]} (octaves {kps['octave'][bad[:5]]})"
+
+
+def test_operator_kd_surface(cases):
+    img, params, ex, kps, desc, orc, okps, odesc = cases["kitti_L"]
+    tuples, d = ex.operator_kd(img)
+    assert isinstance(tuples, list) and isinstance(tuples[0], tuple) and len(tuples[0]) == 6
+    assert all(isinstance(v, float) for v in tuples[0][:5]) and isinstance(tuples[0][5], int)
+    assert d.dtype == np.uint8 and d.shape == (len(tuples), 32)
+    assert np.array_equal(d, odesc)
+    assert tuples[0] == tuple(float(okps[0][f]) for f in ("x", "y", "size", "angle", "response")) + (
+        int(okps[0]["octave"]),)
+
+
+def test_empty_and_featureless_images():
+    ex = ORBextractor(**KITTI)
+    t, d = ex.operator_kd(np.zeros((0, 0), np.uint8))
+    assert t == [] and d.shape == (0, 0)
+    t, d = ex.operator_kd(np.full((376, 1241), 77, np.uint8))  # flat: no FAST corner anywhere
+    assert t == [] and d.shape == (0, 0)
+    with pytest.raises(RuntimeError):
+        ex.operator_kd(np.zeros((10, 10), np.float64))
+
+
+@pytest.mark.parametrize("simd", [0, 32])
+def test_resize_simd_modes(simd):
+    img, _ = synth.make_pair(4)
+    ex = ORBextractor(**KITTI, resize_simd_lanes=simd)
+    kps, desc = ex.extract(img)
+    orc = O.OracleExtractor(**KITTI, resize_simd_lanes=simd)
+    okps, odesc = orc.extract(img)
+    for g, o in zip(ex.GetImagePyramid(sheared=False), orc.pyramid()):
+        assert np.array_equal(g, o)
+    assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
+
+
+def test_deterministic_repeat(cases):
+    img, params, ex, kps, desc, *_ = cases["kitti06"]
+    for _ in range(3):
+        k2, d2 = ex.extract(img)
+        assert k2.tobytes() == kps.tobytes() and np.array_equal(d2, desc)
