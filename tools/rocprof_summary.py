@@ -9,10 +9,11 @@ def rows_from_db(path):
     db = sqlite3.connect(path)
     cur = db.cursor()
     out = []
-    for name, calls, total, avg, pct in cur.execute("select name, total_calls, total_duration, average, percentage "
-                                                    "from top_kernels"):
-        d = list(cur.execute("select min(duration), max(duration) from kernels where name = ?", (name,)))[0]
-        out.append((name, int(calls), float(total), float(avg), float(d[0]), float(d[1]), float(pct)))
+    top = cur.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    for name, calls, total, avg, pct in top:
+        # top_kernels is in microseconds, the per-dispatch `duration` column in nanoseconds
+        d = cur.execute("select min(duration), max(duration) from kernels where name = ?", (name,)).fetchone()
+        out.append((name, int(calls), float(total), float(avg), float(d[0]) / 1e3, float(d[1]) / 1e3, float(pct)))
     return out
 
 
