@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--cpu-sample", type=int, default=24, help="pairs timed for cpu_baseline (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify the last step's pair 0 against the oracle")
+    ap.add_argument("--gather", action="store_true",
+                    help="after timing, gather every pair's results on rank 0 (dist.gather_results, untimed)")
     args = ap.parse_args()
 
     import torch
@@ -106,10 +108,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; the modulo only matters when rehearsing several ranks on one GPU (gloo)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("ORBFE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from pyorbslam_amd import synth
     from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
@@ -145,9 +152,20 @@ def main():
     call("orbfe_profile_read", fe.handle, ms, C.byref(nb))
     stage_ms = {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = t.to(dev) if dist.get_backend() == "nccl" else t
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    gather_s = None
+    if args.gather and world > 1:
+        from pyorbslam_amd import dist as D
+        tg = time.perf_counter()
+        recs = np.stack([D.pack(fe.kp_cap, *fe.fetch_image(2 * p), *fe.fetch_image(2 * p + 1), fe.fetch_stereo(p))
+                         for p in range(P)])
+        allrec = D.gather_results(recs, world * P, device=dev if dist.get_backend() == "nccl" else None)
+        gather_s = time.perf_counter() - tg
+        if rank == 0:
+            assert allrec.shape[0] == world * P
 
     if args.check:
         from oracle.oracle import OracleExtractor
@@ -186,6 +204,8 @@ def main():
                          "pipeline_bytes_per_pair": total_b,
                          "pipeline_frac": round(pairs_per_s / world * total_b / (HBM_PEAK_GBS * 1e9), 6)},
         }
+        if gather_s is not None:
+            out["gather_s_untimed"] = round(gather_s, 4)
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
         else:

@@ -166,6 +166,13 @@ int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_qu
                          int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* best_dist,
                          int32_t* best_idx, int32_t* second_dist, int32_t* second_idx);
 
+/* Every candidate distance, in CSR order: out_dist[k] = popcount(query[q] ^ train[cand_idx[k]]) for
+ * k in [cand_off[q], cand_off[q+1]).  Used by the ORBMatcher drop-in, whose control flow (already
+ * matched points, stereo gate, best/second bookkeeping) depends on matches made earlier in the
+ * same search and therefore stays sequential on the host. */
+int orbfe_hamming_csr(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
+                      int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* out_dist);
+
 /* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);

@@ -706,38 +706,62 @@ int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, con
     });
 }
 
+namespace {
+// shared body of orbfe_hamming_search / orbfe_hamming_csr
+void hamming_run(orbfe_ctx& c, const uint8_t* q, int nq, const uint8_t* t, int nt, const int32_t* off,
+                 const int32_t* idx, std::vector<int>* top2, int32_t* all_d) {
+    if (nq < 0 || nt < 0) throw Error(ORBFE_EINVAL, "negative size");
+    if (nq == 0) return;
+    if (off[0] != 0) throw Error(ORBFE_EINVAL, "cand_off[0] must be 0");
+    for (int i = 0; i < nq; ++i)
+        if (off[i + 1] < off[i]) throw Error(ORBFE_EINVAL, "cand_off must be non-decreasing");
+    const int ncand = off[nq];
+    for (int i = 0; i < ncand; ++i)
+        if (idx[i] < 0 || idx[i] >= nt) throw Error(ORBFE_EINVAL, "candidate index out of range");
+    hipStream_t s = own(c);
+    c.d_hq.ensure((size_t)nq * 32);
+    c.d_ht.ensure((size_t)std::max(nt, 1) * 32);
+    c.d_hoff.ensure((size_t)nq + 1);
+    c.d_hidx.ensure((size_t)std::max(ncand, 1));
+    c.d_hres.ensure((size_t)4 * nq + std::max(ncand, 1));
+    HIPCK(hipMemcpyAsync(c.d_hq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    if (nt) HIPCK(hipMemcpyAsync(c.d_ht.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, s));
+    HIPCK(hipMemcpyAsync(c.d_hoff.p, off, ((size_t)nq + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    if (ncand) HIPCK(hipMemcpyAsync(c.d_hidx.p, idx, (size_t)ncand * sizeof(int), hipMemcpyHostToDevice, s));
+    int* r = c.d_hres.p;
+    int* dall = all_d ? r + 4 * nq : nullptr;
+    HIPCK(launch_hamming_search(c.d_hq.p, nq, c.d_ht.p, c.d_hoff.p, c.d_hidx.p, r, r + nq, r + 2 * nq, r + 3 * nq, dall,
+                                s));
+    if (top2) {
+        top2->resize((size_t)4 * nq);
+        HIPCK(hipMemcpyAsync(top2->data(), r, top2->size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    }
+    if (all_d && ncand) HIPCK(hipMemcpyAsync(all_d, dall, (size_t)ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCK(hipStreamSynchronize(s));
+}
+}  // namespace
+
 int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
                          int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* best_dist,
                          int32_t* best_idx, int32_t* second_dist, int32_t* second_idx) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
-        if (n_query < 0 || n_train < 0) throw Error(ORBFE_EINVAL, "negative size");
-        if (n_query == 0) return;
-        const int ncand = cand_off[n_query];
-        for (int i = 0; i < ncand; ++i)
-            if (cand_idx[i] < 0 || cand_idx[i] >= n_train) throw Error(ORBFE_EINVAL, "candidate index out of range");
-        hipStream_t s = own(*h);
-        h->d_hq.ensure((size_t)n_query * 32);
-        h->d_ht.ensure((size_t)std::max(n_train, 1) * 32);
-        h->d_hoff.ensure((size_t)n_query + 1);
-        h->d_hidx.ensure((size_t)std::max(ncand, 1));
-        h->d_hres.ensure((size_t)4 * n_query + std::max(ncand, 1));
-        HIPCK(hipMemcpyAsync(h->d_hq.p, query_desc, (size_t)n_query * 32, hipMemcpyHostToDevice, s));
-        if (n_train) HIPCK(hipMemcpyAsync(h->d_ht.p, train_desc, (size_t)n_train * 32, hipMemcpyHostToDevice, s));
-        HIPCK(hipMemcpyAsync(h->d_hoff.p, cand_off, ((size_t)n_query + 1) * sizeof(int), hipMemcpyHostToDevice, s));
-        if (ncand) HIPCK(hipMemcpyAsync(h->d_hidx.p, cand_idx, (size_t)ncand * sizeof(int), hipMemcpyHostToDevice, s));
-        int* r = h->d_hres.p;
-        HIPCK(launch_hamming_search(h->d_hq.p, n_query, h->d_ht.p, h->d_hoff.p, h->d_hidx.p, r, r + n_query,
-                                    r + 2 * n_query, r + 3 * n_query, nullptr, s));
-        std::vector<int> res((size_t)4 * n_query);
-        HIPCK(hipMemcpyAsync(res.data(), r, res.size() * sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCK(hipStreamSynchronize(s));
+        std::vector<int> res;
+        hamming_run(*h, query_desc, n_query, train_desc, n_train, cand_off, cand_idx, &res, nullptr);
         for (int i = 0; i < n_query; ++i) {
             if (best_dist) best_dist[i] = res[i];
             if (best_idx) best_idx[i] = res[n_query + i];
             if (second_dist) second_dist[i] = res[2 * n_query + i];
             if (second_idx) second_idx[i] = res[3 * n_query + i];
         }
+    });
+}
+
+int orbfe_hamming_csr(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
+                      int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* out_dist) {
+    return guarded([&] {
+        if (!h || !out_dist) throw Error(ORBFE_EINVAL, "null argument");
+        hamming_run(*h, query_desc, n_query, train_desc, n_train, cand_off, cand_idx, nullptr, out_dist);
     });
 }
 

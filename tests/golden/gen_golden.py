@@ -133,7 +133,7 @@ def gen_stereo(RFrame):
 class MP:
     """Stand-in MapPoint exposing only what search_by_projection_f_p / _f_f read."""
 
-    def __init__(self, desc, pos=None, in_view=True, proj=(0.0, 0.0, 0.0), level=0, view_cos=1.0, bad=False, obs=0):
+    def __init__(self, desc, pos=None, in_view=True, proj=(0.0, 0.0, 0.0), level=0, view_cos=1.0, bad=False, obs=2):
         self._d = desc
         self._p = pos
         self.mbTrackInView = in_view
@@ -147,32 +147,36 @@ class MP:
         return self._bad
 
     def get_descriptor(self):
-        return self._d
+        return self._d.copy()
 
     def get_world_pos(self):
-        return self._p
+        return self._p.copy()
 
     def observations(self):
         return self._obs
 
 
-class GridFrame:
-    """Stand-in Frame: grid bookkeeping as Frame.assign_features_to_grid / get_features_in_area."""
+def make_frame_arrays(rng, n, w=1241, h=376):
+    return dict(x=rng.uniform(20, w - 20, n).astype(np.float32), y=rng.uniform(20, h - 20, n).astype(np.float32),
+                octave=rng.integers(0, 8, n).astype(np.int32), angle=rng.uniform(0, 360, n).astype(np.float32),
+                desc=rng.integers(0, 256, (n, 32), dtype=np.uint8),
+                uR=np.where(rng.random(n) < 0.3, -1.0, 0.0).astype(np.float32))
 
-    def __init__(self, RFrame, rng, n, w=1241, h=376, scale=None):
-        scale = scale or [1.2 ** l for l in range(8)]
+
+class GridFrame:
+    """Stand-in Frame built from arrays; grid bookkeeping and get_features_in_area are the REFERENCE's
+    methods (Frame.py:143-159, 373-416) bound to this object."""
+
+    def __init__(self, RFrame, a, w=1241, h=376):
+        n = len(a["x"])
         self.N = n
-        xs = rng.uniform(20, w - 20, n).astype(np.float32)
-        ys = rng.uniform(20, h - 20, n).astype(np.float32)
-        octs = rng.integers(0, 8, n)
-        angs = rng.uniform(0, 360, n).astype(np.float32)
-        self.mvKeys = [KP(x, y, o, a) for x, y, o, a in zip(xs, ys, octs, angs)]
+        self.mvKeys = [KP(a["x"][i], a["y"][i], a["octave"][i], a["angle"][i]) for i in range(n)]
         self.mvKeysUn = self.mvKeys
-        self.mDescriptors = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-        self.mvuRight = [(-1 if rng.random() < 0.3 else float(np.float32(x - rng.uniform(1, 60)))) for x in xs]
+        self.mDescriptors = a["desc"]
+        self.mvuRight = [(-1 if a["uR"][i] < 0 else np.float32(a["uR"][i])) for i in range(n)]
         self.mvpMapPoints = [None] * n
         self.mvbOutlier = [False] * n
-        self.mvScaleFactors = [float(np.float32(s)) for s in scale]
+        self.mvScaleFactors = [float(np.float32(1.2) ** 0)] + [float(v) for v in np.cumprod([np.float32(1.2)] * 7)]
         self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = 0.0, float(w), 0.0, float(h)
         self.FRAME_GRID_COLS, self.FRAME_GRID_ROWS = 64, 48
         self.mfGridElementWidthInv = 64.0 / w
@@ -180,63 +184,140 @@ class GridFrame:
         self.fx = self.fy = FX
         self.cx, self.cy = 607.1928, 185.2157
         self.mbf = BF
-        self.mb = BF / FX
-        self.mK = None
+        mK = np.eye(3, dtype=np.float32)
+        mK[0, 0] = FX
+        self.mb = self.mbf / mK[0][0]
         self._ref = RFrame.Frame
-        self.mGrid = [[[] for _ in range(48)] for _ in range(64)]
-        for i, k in enumerate(self.mvKeys):
-            px = round((k.pt[0] - self.mnMinX) * self.mfGridElementWidthInv)
-            py = round((k.pt[1] - self.mnMinY) * self.mfGridElementHeightInv)
-            if 0 <= px < 64 and 0 <= py < 48:
-                self.mGrid[px][py].append(i)
+        RFrame.Frame.assign_features_to_grid(self)
+
+    def pos_in_grid(self, kps):
+        return self._ref.pos_in_grid(self, kps)
 
     def get_features_in_area(self, x, y, r, min_level, max_level):
         return self._ref.get_features_in_area(self, x, y, r, min_level, max_level)
 
 
+def pose(rng, t_scale=0.3, rot_scale=0.02):
+    a = rng.normal(0, rot_scale, 3)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    R = np.eye(3) + K + K @ K / 2
+    U, _, Vt = np.linalg.svd(R)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = (U @ Vt).astype(np.float32)
+    T[:3, 3] = rng.normal(0, t_scale, 3).astype(np.float32)
+    return T
+
+
+def noisy(rng, d):
+    d = d.copy()
+    if rng.random() < 0.8:
+        flip = rng.integers(0, 256, 32, dtype=np.uint8) & rng.integers(0, 256, 32, dtype=np.uint8)
+        flip &= rng.integers(0, 256, 32, dtype=np.uint8)
+        return d ^ flip
+    return rng.integers(0, 256, 32, dtype=np.uint8)
+
+
 def gen_matcher(RFrame, RMatcher):
     rng = np.random.Generator(np.random.PCG64(20251015))
     m = RMatcher.ORBMatcher(0.8, True)
-    # descriptor_distance known answers
     a = rng.integers(0, 256, (256, 32), dtype=np.uint8)
     b = rng.integers(0, 256, (256, 32), dtype=np.uint8)
     b[:8] = a[:8]
     b[8:16] = 255 - a[8:16]
     dd = [int(m.descriptor_distance(a[i], b[i])) for i in range(256)]
     np.savez_compressed(GOLD / "matcher_distance.npz", a=a, b=b, dist=np.array(dd, np.int32))
-    cases = []
+    counts = []
+    # ---- search_by_projection_f_p (ORBMatcher.py:215-283)
     for case in range(6):
-        fr = GridFrame(RFrame, rng, 1500)
+        fa = make_frame_arrays(rng, 1500)
+        fa["uR"] = np.where(fa["uR"] < 0, -1.0, fa["x"] - rng.uniform(1, 60, 1500)).astype(np.float32)
+        fr = GridFrame(RFrame, fa)
         nmp = 600
-        mps, queries = [], []
+        q = dict(desc=np.zeros((nmp, 32), np.uint8), proj=np.zeros((nmp, 3), np.float64),
+                 level=np.zeros(nmp, np.int32), view_cos=np.zeros(nmp), in_view=np.zeros(nmp, bool),
+                 bad=np.zeros(nmp, bool), obs=np.zeros(nmp, np.int32))
+        mps = []
         for j in range(nmp):
             i = int(rng.integers(0, fr.N))
             k = fr.mvKeys[i]
-            d = fr.mDescriptors[i].copy()
-            flip = rng.integers(0, 256, 32, dtype=np.uint8) & rng.integers(0, 256, 32, dtype=np.uint8)
-            flip &= rng.integers(0, 256, 32, dtype=np.uint8)
-            d ^= flip if rng.random() < 0.8 else rng.integers(0, 256, 32, dtype=np.uint8)
-            px = float(k.pt[0] + rng.normal(0, 2))
-            py = float(k.pt[1] + rng.normal(0, 2))
-            pxr = px - float(rng.uniform(0, 40))
-            lvl = int(np.clip(k.octave + rng.integers(-1, 2), 0, 7))
-            vc = float(rng.choice([0.999, 0.5]))
-            mp = MP(d, in_view=bool(rng.random() < 0.95), proj=(px, py, pxr), level=lvl, view_cos=vc,
-                    bad=bool(rng.random() < 0.03))
-            mps.append(mp)
-            queries.append(dict(desc=d.tolist(), proj=[px, py, pxr], level=lvl, view_cos=vc, in_view=mp.mbTrackInView,
-                                bad=mp._bad))
+            q["desc"][j] = noisy(rng, fr.mDescriptors[i])
+            px, py = float(k.pt[0] + rng.normal(0, 2)), float(k.pt[1] + rng.normal(0, 2))
+            q["proj"][j] = (px, py, px - float(rng.uniform(0, 40)))
+            q["level"][j] = int(np.clip(k.octave + rng.integers(-1, 2), 0, 7))
+            q["view_cos"][j] = float(rng.choice([0.999, 0.5]))
+            q["in_view"][j] = bool(rng.random() < 0.95)
+            q["bad"][j] = bool(rng.random() < 0.03)
+            q["obs"][j] = int(rng.choice([0, 1, 3]))
+            mps.append(MP(q["desc"][j], in_view=bool(q["in_view"][j]), proj=tuple(float(v) for v in q["proj"][j]),
+                          level=int(q["level"][j]), view_cos=float(q["view_cos"][j]), bad=bool(q["bad"][j]),
+                          obs=int(q["obs"][j])))
         th = [1.0, 3.0, 5.0][case % 3]
         n = m.search_by_projection_f_p(fr, mps, th)
-        assigned = [(-1 if p is None else mps.index(p)) for p in fr.mvpMapPoints]
-        cases.append(dict(kind="f_p", th=th, n_matches=n, assigned=assigned, queries=queries,
-                          frame=dict(x=[k.pt[0] for k in fr.mvKeys], y=[k.pt[1] for k in fr.mvKeys],
-                                     octave=[k.octave for k in fr.mvKeys], angle=[k.angle for k in fr.mvKeys],
-                                     desc=fr.mDescriptors.tolist(),
-                                     uR=[(None if v == -1 else v) for v in fr.mvuRight])))
-    (GOLD / "matcher_f_p.json").write_text(json.dumps(dict(
-        nnratio=0.8, source="ORBMatcher.search_by_projection_f_p (ORBMatcher.py:215-283)", cases=cases)))
-    print("matcher goldens:", [c["n_matches"] for c in cases])
+        assigned = np.array([(-1 if p is None else mps.index(p)) for p in fr.mvpMapPoints], np.int32)
+        np.savez_compressed(GOLD / f"matcher_fp_{case}.npz", th=th, n_matches=n, assigned=assigned,
+                            **{f"frame_{k}": v for k, v in fa.items()}, **{f"mp_{k}": v for k, v in q.items()})
+        counts.append(n)
+    # ---- search_by_projection_f_f (ORBMatcher.py:291-393)
+    for case in range(6):
+        ca = make_frame_arrays(rng, 1500)
+        cur = GridFrame(RFrame, ca)
+        Tc = pose(rng)
+        # forward / backward / sideways motion relative to the last frame (b_forward / b_backward)
+        dz = [0.0, 0.9, -0.9][case % 3]
+        Tl = Tc.copy()
+        Tl[2, 3] += np.float32(dz)
+        cur.mTcw = Tc
+        nl = 1200
+        la = make_frame_arrays(rng, nl)
+        last = GridFrame(RFrame, la)
+        last.mTcw = Tl
+        Rcw, tcw = Tc[:3, :3].astype(np.float64), Tc[:3, 3].astype(np.float64)
+        mpos = np.zeros((nl, 3), np.float32)
+        mdesc = np.zeros((nl, 32), np.uint8)
+        has = np.zeros(nl, bool)
+        outl = np.zeros(nl, bool)
+        obs = np.zeros(nl, np.int32)
+        for i in range(nl):
+            if rng.random() < 0.15:
+                continue
+            j = int(rng.integers(0, cur.N))
+            k = cur.mvKeys[j]
+            z = float(rng.uniform(3, 40))
+            u, v = k.pt[0] + rng.normal(0, 3), k.pt[1] + rng.normal(0, 3)
+            pc = np.array([(u - cur.cx) * z / FX, (v - cur.cy) * z / FX, z])
+            mpos[i] = (Rcw.T @ (pc - tcw)).astype(np.float32)
+            mdesc[i] = noisy(rng, cur.mDescriptors[j])
+            has[i] = True
+            outl[i] = rng.random() < 0.05
+            obs[i] = int(rng.choice([1, 2, 3]))
+        mps = [MP(mdesc[i], pos=mpos[i].reshape(3, 1), obs=int(obs[i])) if has[i] else None for i in range(nl)]
+        last.mvpMapPoints = mps
+        last.mvbOutlier = [bool(v) for v in outl]
+        # some current keypoints already hold map points (with and without observations)
+        pre = np.full(cur.N, -1, np.int32)
+        pre_obs = np.zeros(cur.N, np.int32)
+        extra = []
+        for j in rng.choice(cur.N, 60, replace=False):
+            pre_obs[j] = int(rng.choice([0, 2]))
+            extra.append(MP(cur.mDescriptors[j], pos=np.zeros((3, 1), np.float32), obs=int(pre_obs[j])))
+            pre[j] = len(extra) - 1
+            cur.mvpMapPoints[j] = extra[-1]
+        th = [7.0, 15.0][case % 2]
+        n = m.search_by_projection_f_f(cur, last, th)
+        assigned = []
+        for p in cur.mvpMapPoints:
+            if p is None:
+                assigned.append(-1)
+            elif p in extra:
+                assigned.append(-2 - extra.index(p))
+            else:
+                assigned.append(mps.index(p))
+        np.savez_compressed(GOLD / f"matcher_ff_{case}.npz", th=th, n_matches=n, assigned=np.array(assigned, np.int32),
+                            Tc=Tc, Tl=Tl, mp_pos=mpos, mp_desc=mdesc, mp_has=has, mp_outlier=outl, mp_obs=obs,
+                            pre=pre, pre_obs=pre_obs, **{f"cur_{k}": v for k, v in ca.items()},
+                            **{f"last_{k}": v for k, v in la.items()})
+        counts.append(n)
+    print("matcher goldens:", counts)
 
 
 def main():

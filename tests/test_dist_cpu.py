@@ -1,0 +1,83 @@
+"""N > 1 path on the CPU: shard plan, record packing, and the rank-0 gather over gloo (world size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from pyorbslam_amd import dist as D
+from pyorbslam_amd._lib import KP_DTYPE
+
+
+def test_shard_plan_covers_all_pairs():
+    for n in (0, 1, 7, 64, 65):
+        for w in (1, 2, 3, 8):
+            spans = [D.shard(n, w, r) for r in range(w)]
+            assert sum(c for _, c in spans) == n
+            assert [s for s, _ in spans] == [sum(c for _, c in spans[:r]) for r in range(w)]
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def _fake(rng, cap, n):
+    k = np.zeros(n, KP_DTYPE)
+    k["x"] = rng.uniform(0, 1000, n)
+    k["octave"] = rng.integers(0, 8, n)
+    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    st = dict(u_right=rng.uniform(0, 100, n).astype(np.float32), depth=rng.uniform(1, 50, n).astype(np.float32),
+              status=rng.integers(0, 3, n).astype(np.int8))
+    return k, d, st
+
+
+def test_pack_unpack_roundtrip():
+    rng = np.random.default_rng(0)
+    cap = 50
+    kl, dl, st = _fake(rng, cap, 37)
+    kr, dr, _ = _fake(rng, cap, 12)
+    rec = D.pack(cap, kl, dl, kr, dr, st)
+    assert rec.size == D.record_bytes(cap)
+    u = D.unpack(cap, rec)
+    assert u["kps_left"].tobytes() == kl.tobytes() and u["kps_right"].tobytes() == kr.tobytes()
+    assert np.array_equal(u["desc_left"], dl) and np.array_equal(u["desc_right"], dr)
+    for k in ("u_right", "depth", "status"):
+        assert np.array_equal(u[k], st[k])
+
+
+def _worker(rank, world, port, n_pairs, cap, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    start, cnt = D.shard(n_pairs, world, rank)
+    recs = []
+    for p in range(start, start + cnt):
+        rng = np.random.default_rng(1000 + p)
+        kl, dl, st = _fake(rng, cap, 10 + p)
+        kr, dr, _ = _fake(rng, cap, 5 + p)
+        recs.append(D.pack(cap, kl, dl, kr, dr, st))
+    recs = np.stack(recs) if recs else np.zeros((0, D.record_bytes(cap)), np.uint8)
+    out = D.gather_results(recs, n_pairs)
+    if rank == 0:
+        ok = True
+        for p in range(n_pairs):
+            rng = np.random.default_rng(1000 + p)
+            kl, dl, st = _fake(rng, cap, 10 + p)
+            u = D.unpack(cap, out[p])
+            ok &= u["kps_left"].tobytes() == kl.tobytes() and np.array_equal(u["u_right"], st["u_right"])
+        q.put(bool(ok) and len(out) == n_pairs)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_pairs", [5, 8])
+def test_gather_world_size_2_gloo(n_pairs):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_pairs, 40, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get() is True

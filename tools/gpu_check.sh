@@ -19,6 +19,11 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   stage bench 600 python bench.py --steps 10 --warmup 3 --cpu-sample 2
 fi
+if [ "$MODE" = dist2 ]; then
+  # rehearse the N>1 path on one GPU: 2 ranks over gloo on cuda:0 (never the N=8 case)
+  ORBFE_DIST_BACKEND=gloo stage dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --pairs 16 --gather
+fi
 if [ "$MODE" = prof ]; then
   export TMPDIR=/tmp
   stage rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 --cpu-sample 0
