@@ -186,6 +186,12 @@ int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, con
 int orbfe_profile_begin(orbfe_handle h, int32_t max_batches);
 int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches);
 
+/* Kernel micro-benchmark on the inputs of the last batch (development aid, not part of the drop-in):
+ * runs stage `stage` (0 resize, 1 detect, 2 octree, 3 describe, 4 stereo) in ablation variant `variant`
+ * (0 = production kernel) `reps` times on the handle's last stream and returns the average ms.
+ * Variants other than 0 overwrite stage outputs with garbage: re-run the batch afterwards. */
+int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t reps, float* ms);
+
 /* ---- diagnostics (stage outputs of the last orbfe_extract, image 0) ------------------------------
  * orbfe_debug_candidates: the level's FAST cell output in vToDistributeKeys order
  *   (ORBextractor.cpp:808-824), as (x_rel, y_rel, score) triples relative to (minBorderX, minBorderY).

@@ -59,6 +59,7 @@ SIGNATURES = {
     "orbfe_hamming_matrix": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p],
     "orbfe_profile_begin": [C.c_void_p, C.c_int32],
     "orbfe_profile_read": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],
+    "orbfe_microbench": [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)],
     "orbfe_debug_candidates": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
 }

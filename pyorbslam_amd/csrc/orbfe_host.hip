@@ -132,6 +132,8 @@ struct orbfe_ctx {
     const uint8_t* last_in = nullptr;  // device input of the last extraction
     int64_t last_pitch = 0;
     int last_images = 0, last_pairs = 0;
+    double last_bf = 0.0;
+    float last_fx = 0.f;
     bool have_single = false;          // orbfe_extract ran and its buffers are valid
 
     ~orbfe_ctx() {
@@ -298,6 +300,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
                     if (rw > kMaxCellRoi || rh > kMaxCellRoi) throw Error(ORBFE_EINVAL, "FAST cell larger than 64 px");
                     const int ww = std::max(rw - 6, 0), wh = std::max(rh - 6, 0);
+                    g.max_roi = std::max(g.max_roi, (rw * rh + 15) & ~15);
+                    g.max_win = std::max(g.max_win, (ww * wh + 15) & ~15);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
                     slot_off += cg.slot_cap;
@@ -448,6 +452,8 @@ void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStr
     a.match_r = c.d_match.p;
     a.out_stride = g.kp_cap;
     stereo_consts(bf, fx, a);
+    c.last_bf = bf;
+    c.last_fx = fx;
     HIPCK(launch_stereo(g, a, n_pairs, s));
     prof_mark(c, s, 5);
     if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
@@ -795,6 +801,56 @@ int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches) 
         }
         if (n_batches) *n_batches = h->prof_n;
         h->prof_on = false;
+    });
+}
+
+int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t reps, float* ms) {
+    return guarded([&] {
+        if (!h || !ms || reps <= 0) throw Error(ORBFE_EINVAL, "bad argument");
+        if (h->last_images <= 0 || !h->last_in) throw Error(ORBFE_ESTATE, "run a batch first");
+        const Geo& g = h->geo;
+        const int n = h->last_images;
+        hipStream_t s = h->last_stream;
+        hipEvent_t e0, e1;
+        HIPCK(hipEventCreate(&e0));
+        HIPCK(hipEventCreate(&e1));
+        auto run = [&] {
+            switch (stage) {
+                case 0:
+                    for (int l = 1; l < g.nlevels; ++l)
+                        HIPCK(launch_resize(g, l, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, n, s));
+                    break;
+                case 1:
+                    HIPCK(launch_detect(g, h->d_cells.p, h->last_in, h->last_pitch, h->d_ws.p, h->d_cell_count.p,
+                                        h->d_slots.p, n, s, variant));
+                    break;
+                case 2:
+                    HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_kd.p, h->d_kn.p,
+                                        h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s));
+                    break;
+                case 3:
+                    HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
+                                          h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_chunk_level.p,
+                                          (int)h->chunk_level.size(), n, s));
+                    break;
+                case 4:
+                    if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");
+                    enqueue_stereo_batch(*h, h->last_pairs, h->last_bf, h->last_fx, s);
+                    break;
+                default:
+                    throw Error(ORBFE_EINVAL, "bad stage");
+            }
+        };
+        run();  // warm
+        HIPCK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) run();
+        HIPCK(hipEventRecord(e1, s));
+        HIPCK(hipEventSynchronize(e1));
+        float t = 0.f;
+        HIPCK(hipEventElapsedTime(&t, e0, e1));
+        *ms = t / reps;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
     });
 }
 

@@ -165,83 +165,140 @@ __device__ __forceinline__ int fast_m(const uint8_t* r, int s) {
     return max(max(v - lo, hi - v), 0);
 }
 
-// One workgroup per (cell, image).  Output: the cell's keypoints in FAST's row-major order packed as
-// x | y << 12 | score << 24 (level coordinates), and the per-cell count.
-__global__ __launch_bounds__(256) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
-                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
-                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
-    __shared__ uint8_t roi[kMaxCellRoi * kMaxCellRoi];
-    __shared__ uint8_t mm[kMaxCellRoi * kMaxCellRoi];
-    __shared__ int red[8];
-    __shared__ int cnts[256];
-    __shared__ int scan_tmp[257];
-    const int c = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+// Advance a flattened row-major index by 64 inside a `w`-wide window without dividing.
+__device__ __forceinline__ void step64(int& y, int& x, int w) {
+    x += 64;
+    while (x >= w) {
+        x -= w;
+        ++y;
+    }
+}
+
+// One wavefront per (cell, image).  The cell ROI is staged in LDS; every window pixel gets a cheap
+// necessary test for "M > t" at t = min(iniTh, minTh): an arc of 9 contiguous circle pixels always
+// contains two circularly adjacent cardinal pixels (0,4,8,12), so both of them must be darker than
+// v - t (or both brighter than v + t).  Pixels that fail have M <= t, i.e. they are neither corners
+// nor non-zero NMS neighbours at either threshold, and get M = 0.  Survivors are compacted (ballot +
+// mbcnt) into an LDS queue and their exact M is computed by fully occupied lanes.  NMS and the
+// ordered compaction into the cell slot then run 64 window pixels per step in row-major order, so the
+// slot order is FAST's output order with no block-wide scan.
+// Output: x | y << 12 | score << 24 (level coordinates) per keypoint, and the per-cell count.
+template <int V>
+__global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
+                                               int64_t in_pitch, const uint8_t* __restrict__ ws,
+                                               int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    uint16_t* queue = (uint16_t*)lds;                 // max_win entries
+    uint8_t* roi = lds + 2 * g.max_win;               // max_roi bytes
+    uint8_t* mm = roi + g.max_roi;                    // max_win bytes
+    const int c = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
     const CellGeo cg = cells[c];
     int stride;
     const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
-    for (int i = t; i < rw * rh; i += 256) {
-        const int y = i / rw, x = i - y * rw;
-        roi[i] = lvl[(int64_t)(cg.y0 + y) * stride + cg.x0 + x];
+    {
+        int y = 0, x = lane;
+        while (x >= rw) { x -= rw; ++y; }
+        const uint8_t* src = lvl + (int64_t)cg.y0 * stride + cg.x0;
+        for (int i = lane; i < rw * rh; i += 64) {
+            roi[i] = src[(int64_t)y * stride + x];
+            step64(y, x, rw);
+        }
     }
     __syncthreads();
+    if (V == 1) {  // ablation: ROI staging only
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = roi[rw * rh / 2] & 0;
+        return;
+    }
     const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
     const int npx = (ww > 0 && wh > 0) ? ww * wh : 0;
-    for (int i = t; i < npx; i += 256) {
-        const int y = i / ww, x = i - y * ww;
+    const int tq = min(g.ini_th, g.min_th);
+    // pass A: cardinal pre-test, M = 0 for rejected pixels, queue the rest
+    int nq = 0;
+    {
+        int y = 0, x = lane;
+        while (ww > 0 && x >= ww) { x -= ww; ++y; }
+        for (int base = 0; base < npx; base += 64) {
+            const int i = base + lane;
+            bool cand = false;
+            if (i < npx) {
+                const uint8_t* r = roi + (y + 3) * rw + x + 3;
+                const int v = r[0], lo = v - tq, hi = v + tq;
+                const int c0 = r[3 * rw], c1 = r[3], c2 = r[-3 * rw], c3 = r[-3];
+                const bool d0 = c0 < lo, d1 = c1 < lo, d2 = c2 < lo, d3 = c3 < lo;
+                const bool b0 = c0 > hi, b1 = c1 > hi, b2 = c2 > hi, b3 = c3 > hi;
+                cand = (d0 & d1) | (d1 & d2) | (d2 & d3) | (d3 & d0) | (b0 & b1) | (b1 & b2) | (b2 & b3) | (b3 & b0);
+                mm[i] = 0;
+                step64(y, x, ww);
+            }
+            const uint64_t bal = __ballot(cand);
+            if (cand) queue[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)i;
+            nq += __popcll(bal);
+        }
+    }
+    __syncthreads();
+    if (V == 2) {  // ablation: + pre-test / queue
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nq & 0;
+        return;
+    }
+    // pass B: exact M of the queued pixels, all lanes busy
+    for (int k = lane; k < nq; k += 64) {
+        const int i = queue[k];
+        int y = 0, x = i;
+        // one division per survivor (survivors are a minority)
+        y = i / ww;
+        x = i - y * ww;
         mm[i] = (uint8_t)fast_m(roi + (y + 3) * rw + x + 3, rw);
     }
     __syncthreads();
-    // thread-contiguous chunks in row-major order keep the compaction in FAST's output order
-    const int per = (npx + 255) >> 8;  // <= 14 for a 58x58 window
-    const int b = min(t * per, npx), e = min(b + per, npx);
-    int th = g.ini_th;
-    uint64_t keep_mask = 0;
-    int cnt = 0, total = 0;
+    if (V == 3) {  // ablation: + exact M
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = mm[npx / 2] & 0;
+        return;
+    }
+    uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
+    int th = g.ini_th, total = 0;
     for (int pass = 0; pass < 2; ++pass) {
-        keep_mask = 0;
-        cnt = 0;
-        for (int i = b; i < e; ++i) {
-            const int m = mm[i];
-            if (m <= th) continue;
-            const int s = m - 1;
-            const int y = i / ww, x = i - y * ww;
-            bool keep = true;
+        total = 0;
+        int y = 0, x = lane;
+        while (ww > 0 && x >= ww) { x -= ww; ++y; }
+        for (int base = 0; base < npx; base += 64) {
+            const int i = base + lane;
+            bool keep = false;
+            int s = 0, px = x, py = y;
+            if (i < npx) {
+                const int m = mm[i];
+                if (m > th) {
+                    s = m - 1;
+                    keep = true;
 #pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
+                    for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (!dx && !dy) continue;
-                    const int yy = y + dy, xx = x + dx;
-                    int sq = 0;  // outside the window or not a corner at th: score 0
-                    if (yy >= 0 && yy < wh && xx >= 0 && xx < ww) {
-                        const int mq = mm[yy * ww + xx];
-                        sq = mq > th ? mq - 1 : 0;
-                    }
-                    keep = keep && (s > sq);
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            if (!dx && !dy) continue;
+                            const int yy = y + dy, xx = x + dx;
+                            int sq = 0;  // outside the window or not a corner at th: score 0
+                            if (yy >= 0 && yy < wh && xx >= 0 && xx < ww) {
+                                const int mq = mm[yy * ww + xx];
+                                sq = mq > th ? mq - 1 : 0;
+                            }
+                            keep = keep && (s > sq);
+                        }
                 }
-            if (keep) {
-                keep_mask |= 1ull << (i - b);
-                ++cnt;
+                step64(y, x, ww);
             }
+            const uint64_t bal = __ballot(keep);
+            if (keep) {
+                const int o = total + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+                if (o < cg.slot_cap)
+                    out[o] = (uint32_t)(cg.x0 + px + 3) | ((uint32_t)(cg.y0 + py + 3) << 12) | ((uint32_t)s << 24);
+            }
+            total += __popcll(bal);
         }
-        total = block_sum(cnt, red);
         if (total > 0) break;
         th = g.min_th;  // empty cell at iniThFAST: retry at minThFAST (ORBextractor.cpp:811-815)
     }
-    cnts[t] = cnt;
-    __syncthreads();
-    block_excl_scan(cnts, 256, scan_tmp);
-    uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-    int o = cnts[t];
-    for (int i = b; i < e; ++i) {
-        if (!((keep_mask >> (i - b)) & 1ull)) continue;
-        const int y = i / ww, x = i - y * ww;
-        const uint32_t X = (uint32_t)(cg.x0 + x + 3), Y = (uint32_t)(cg.y0 + y + 3), S = (uint32_t)(mm[i] - 1);
-        if (o < cg.slot_cap) out[o] = X | (Y << 12) | (S << 24);  // bound holds by NMS; never write past it
-        ++o;
-    }
-    if (t == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
+    if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
 }
 
 // ------------------------------------------------------------------------------- k_octree
@@ -970,9 +1027,15 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 }
 
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
-                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s) {
-    hipLaunchKernelGGL(k_detect, dim3(g.ncells, n_images), dim3(256), 0, s, g, cells, in, in_pitch, ws, cell_count,
-                       slots);
+                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
+    const size_t lds = (size_t)3 * g.max_win + g.max_roi;
+    const dim3 grid(g.ncells, n_images), blk(64);
+    switch (variant) {
+        case 1: hipLaunchKernelGGL(k_detect<1>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
+        case 2: hipLaunchKernelGGL(k_detect<2>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
+        case 3: hipLaunchKernelGGL(k_detect<3>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
+        default: hipLaunchKernelGGL(k_detect<0>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
+    }
     return hipGetLastError();
 }
 
