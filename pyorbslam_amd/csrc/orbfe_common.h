@@ -73,7 +73,8 @@ struct Geo {
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count
     int max_ncap;        // octree node capacity (max over levels of kp_cap)
-    int max_roi;         // largest FAST cell ROI (pixels), rounded up to 16
+    int max_rh;          // largest FAST cell ROI height (rows)
+    int max_wh;          // largest FAST detection window height (rows)
     int max_win;         // largest FAST detection window (pixels), rounded up to 16
     int umax[16];
     float scale[kMaxLevels];

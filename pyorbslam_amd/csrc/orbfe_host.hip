@@ -298,9 +298,11 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     cg.x1 = (int16_t)(int)maxXc;
                     cg.y1 = (int16_t)(int)maxYc;
                     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
-                    if (rw > kMaxCellRoi || rh > kMaxCellRoi) throw Error(ORBFE_EINVAL, "FAST cell larger than 64 px");
+                    // k_detect stages a ROI row as 16 re-aligned dwords (<= 64 px)
+                    if (rw > 64 || rh > 64) throw Error(ORBFE_EINVAL, "FAST cell ROI larger than 64 px");
                     const int ww = std::max(rw - 6, 0), wh = std::max(rh - 6, 0);
-                    g.max_roi = std::max(g.max_roi, (rw * rh + 15) & ~15);
+                    g.max_rh = std::max(g.max_rh, rh);
+                    g.max_wh = std::max(g.max_wh, wh);
                     g.max_win = std::max(g.max_win, (ww * wh + 15) & ~15);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);

@@ -165,138 +165,147 @@ __device__ __forceinline__ int fast_m(const uint8_t* r, int s) {
     return max(max(v - lo, hi - v), 0);
 }
 
-// Advance a flattened row-major index by 64 inside a `w`-wide window without dividing.
-__device__ __forceinline__ void step64(int& y, int& x, int w) {
-    x += 64;
-    while (x >= w) {
-        x -= w;
-        ++y;
-    }
+// FAST "M" on a pitch-64 LDS image: every circle offset is an immediate.
+__device__ __forceinline__ int fast_m64(const uint8_t* r) {
+    return fast_m(r, 64);
 }
 
-// One wavefront per (cell, image).  The cell ROI is staged in LDS; every window pixel gets a cheap
-// necessary test for "M > t" at t = min(iniTh, minTh): an arc of 9 contiguous circle pixels always
-// contains two circularly adjacent cardinal pixels (0,4,8,12), so both of them must be darker than
-// v - t (or both brighter than v + t).  Pixels that fail have M <= t, i.e. they are neither corners
-// nor non-zero NMS neighbours at either threshold, and get M = 0.  Survivors are compacted (ballot +
-// mbcnt) into an LDS queue and their exact M is computed by fully occupied lanes.  NMS and the
-// ordered compaction into the cell slot then run 64 window pixels per step in row-major order, so the
-// slot order is FAST's output order with no block-wide scan.
-// Output: x | y << 12 | score << 24 (level coordinates) per keypoint, and the per-cell count.
+// One wavefront per (cell, image).
+//  1. ROI -> LDS at a fixed pitch of 64 (ROI pixel (r, c) at r*64 + c): each row is read as 17 dwords
+//     from its 4-byte aligned start and re-aligned with v_alignbyte; all loads are issued before the
+//     first wait.
+//  2. Pre-test at t = min(iniTh, minTh): an arc of 9 contiguous circle pixels always contains two
+//     circularly adjacent cardinals (0,4,8,12), so both must be darker than v - t (or both brighter
+//     than v + t).  Failing pixels have M <= t: neither corners nor relevant NMS neighbours at either
+//     threshold; they keep M = 0.  Survivors are compacted (ballot + mbcnt) into an LDS queue.
+//  3. Exact M of the queued pixels, all lanes busy, written into a zero-bordered pitch-64 M map.
+//  4. NMS.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the window or not
+//     corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour with M <= t
+//     is below M anyway.  So the local-max test is threshold independent and the iniTh -> minTh
+//     fallback (ORBextractor.cpp:811-815) only changes the final cut M > max(t, 1).  Kept pixels are
+//     written in row-major order (ballot-ordered), i.e. cv::FAST's output order.
+// Window pixels map to lanes 32 per row when the window is at most 32 wide (2 rows per step), else 64.
 template <int V>
 __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint16_t* queue = (uint16_t*)lds;                 // max_win entries
-    uint8_t* roi = lds + 2 * g.max_win;               // max_roi bytes
-    uint8_t* mm = roi + g.max_roi;                    // max_win bytes
+    uint8_t* roi = lds;                                   // max_rh rows x 64
+    uint8_t* mm = roi + 64 * g.max_rh;                    // (max_wh + 2) rows x 64, zero border
+    uint16_t* queue = (uint16_t*)(mm + 64 * (g.max_wh + 2));  // max_win entries (y << 6 | x)
     const int c = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
     const CellGeo cg = cells[c];
     int stride;
     const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
+    const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
+    // ---- 1. stage the ROI (16 lanes per row, 4 rows per step; up to 16 steps = 64 rows)
     {
-        int y = 0, x = lane;
-        while (x >= rw) { x -= rw; ++y; }
-        const uint8_t* src = lvl + (int64_t)cg.y0 * stride + cg.x0;
-        for (int i = lane; i < rw * rh; i += 64) {
-            roi[i] = src[(int64_t)y * stride + x];
-            step64(y, x, rw);
+        const int d = lane & 15, r0 = lane >> 4;
+        const int ndw = (rw + 3) >> 2;
+        uint32_t lo[16], hi[16];
+        int sh[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int r = r0 + 4 * k;
+            lo[k] = hi[k] = 0;
+            sh[k] = 0;
+            if (r < rh && d < ndw) {
+                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cg.y0 + r) * stride + cg.x0);
+                const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
+                sh[k] = (int)(a & 3);
+                lo[k] = p[d];
+                hi[k] = p[d + 1];
+            }
         }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int r = r0 + 4 * k;
+            if (r < rh && d < ndw)
+                *(uint32_t*)(roi + r * 64 + 4 * d) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+        }
+        // zero the M map (window + 1-pixel border)
+        uint32_t* m32 = (uint32_t*)mm;
+        for (int i = lane; i < 16 * (wh + 2); i += 64) m32[i] = 0u;
     }
     __syncthreads();
     if (V == 1) {  // ablation: ROI staging only
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = roi[rw * rh / 2] & 0;
         return;
     }
-    const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
-    const int npx = (ww > 0 && wh > 0) ? ww * wh : 0;
+    if (ww <= 0 || wh <= 0) {
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = 0;
+        return;
+    }
+    const int lshift = ww <= 32 ? 5 : 6;           // lanes per window row: 32 or 64
+    const int lx = lane & ((1 << lshift) - 1), ly = lane >> lshift, rows_per = 64 >> lshift;
     const int tq = min(g.ini_th, g.min_th);
-    // pass A: cardinal pre-test, M = 0 for rejected pixels, queue the rest
+    // ---- 2. pre-test + queue
     int nq = 0;
-    {
-        int y = 0, x = lane;
-        while (ww > 0 && x >= ww) { x -= ww; ++y; }
-        for (int base = 0; base < npx; base += 64) {
-            const int i = base + lane;
-            bool cand = false;
-            if (i < npx) {
-                const uint8_t* r = roi + (y + 3) * rw + x + 3;
-                const int v = r[0], lo = v - tq, hi = v + tq;
-                const int c0 = r[3 * rw], c1 = r[3], c2 = r[-3 * rw], c3 = r[-3];
-                const bool d0 = c0 < lo, d1 = c1 < lo, d2 = c2 < lo, d3 = c3 < lo;
-                const bool b0 = c0 > hi, b1 = c1 > hi, b2 = c2 > hi, b3 = c3 > hi;
-                cand = (d0 & d1) | (d1 & d2) | (d2 & d3) | (d3 & d0) | (b0 & b1) | (b1 & b2) | (b2 & b3) | (b3 & b0);
-                mm[i] = 0;
-                step64(y, x, ww);
-            }
-            const uint64_t bal = __ballot(cand);
-            if (cand) queue[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)i;
-            nq += __popcll(bal);
+    for (int y0 = 0; y0 < wh; y0 += rows_per) {
+        const int y = y0 + ly;
+        bool cand = false;
+        if (y < wh && lx < ww) {
+            const uint8_t* r = roi + (y + 3) * 64 + lx + 3;
+            const int v = r[0], lo = v - tq, hi = v + tq;
+            const int c0 = r[3 * 64], c1 = r[3], c2 = r[-3 * 64], c3 = r[-3];
+            const bool d0 = c0 < lo, d1 = c1 < lo, d2 = c2 < lo, d3 = c3 < lo;
+            const bool b0 = c0 > hi, b1 = c1 > hi, b2 = c2 > hi, b3 = c3 > hi;
+            cand = (d0 & d1) | (d1 & d2) | (d2 & d3) | (d3 & d0) | (b0 & b1) | (b1 & b2) | (b2 & b3) | (b3 & b0);
         }
+        const uint64_t bal = __ballot(cand);
+        if (cand)
+            queue[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] =
+                (uint16_t)((y << 6) | lx);
+        nq += __popcll(bal);
     }
     __syncthreads();
     if (V == 2) {  // ablation: + pre-test / queue
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nq & 0;
         return;
     }
-    // pass B: exact M of the queued pixels, all lanes busy
+    // ---- 3. exact M of the survivors
     for (int k = lane; k < nq; k += 64) {
-        const int i = queue[k];
-        int y = 0, x = i;
-        // one division per survivor (survivors are a minority)
-        y = i / ww;
-        x = i - y * ww;
-        mm[i] = (uint8_t)fast_m(roi + (y + 3) * rw + x + 3, rw);
+        const int q = queue[k], y = q >> 6, x = q & 63;
+        mm[(y + 1) * 64 + x + 1] = (uint8_t)fast_m64(roi + (y + 3) * 64 + x + 3);
     }
     __syncthreads();
     if (V == 3) {  // ablation: + exact M
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = mm[npx / 2] & 0;
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = mm[65] & 0;
         return;
     }
+    // ---- 4. NMS (local max) + ordered compaction at iniTh, else minTh
     uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-    int th = g.ini_th, total = 0;
+    int total = 0;
+    const int tlow = max(min(g.ini_th, g.min_th), 1);
     for (int pass = 0; pass < 2; ++pass) {
+        const int th = max(pass == 0 ? g.ini_th : g.min_th, 1);
         total = 0;
-        int y = 0, x = lane;
-        while (ww > 0 && x >= ww) { x -= ww; ++y; }
-        for (int base = 0; base < npx; base += 64) {
-            const int i = base + lane;
+        for (int y0 = 0; y0 < wh; y0 += rows_per) {
+            const int y = y0 + ly;
             bool keep = false;
-            int s = 0, px = x, py = y;
-            if (i < npx) {
-                const int m = mm[i];
-                if (m > th) {
-                    s = m - 1;
-                    keep = true;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; ++dx) {
-                            if (!dx && !dy) continue;
-                            const int yy = y + dy, xx = x + dx;
-                            int sq = 0;  // outside the window or not a corner at th: score 0
-                            if (yy >= 0 && yy < wh && xx >= 0 && xx < ww) {
-                                const int mq = mm[yy * ww + xx];
-                                sq = mq > th ? mq - 1 : 0;
-                            }
-                            keep = keep && (s > sq);
-                        }
+            int m = 0;
+            if (y < wh && lx < ww) {
+                const uint8_t* p = mm + (y + 1) * 64 + lx + 1;
+                m = p[0];
+                if (m > th && m > tlow) {
+                    const int n0 = max(max(p[-65], p[-64]), p[-63]);
+                    const int n1 = max(max(p[-1], p[1]), p[63]);
+                    const int n2 = max(p[64], p[65]);
+                    keep = m > max(max(n0, n1), n2);
                 }
-                step64(y, x, ww);
             }
             const uint64_t bal = __ballot(keep);
             if (keep) {
-                const int o = total + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+                const int o = total + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
                 // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
                 if (o < cg.slot_cap)
-                    out[o] = (uint32_t)(cg.x0 + px + 3) | ((uint32_t)(cg.y0 + py + 3) << 12) | ((uint32_t)s << 24);
+                    out[o] = (uint32_t)(cg.x0 + lx + 3) | ((uint32_t)(cg.y0 + y + 3) << 12) | ((uint32_t)(m - 1) << 24);
             }
             total += __popcll(bal);
         }
-        if (total > 0) break;
-        th = g.min_th;  // empty cell at iniThFAST: retry at minThFAST (ORBextractor.cpp:811-815)
+        if (total > 0 || g.min_th == g.ini_th) break;
     }
     if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
 }
@@ -1028,7 +1037,7 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
-    const size_t lds = (size_t)3 * g.max_win + g.max_roi;
+    const size_t lds = (size_t)64 * g.max_rh + 64 * (g.max_wh + 2) + 2 * g.max_win;
     const dim3 grid(g.ncells, n_images), blk(64);
     switch (variant) {
         case 1: hipLaunchKernelGGL(k_detect<1>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
