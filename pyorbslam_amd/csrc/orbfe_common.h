@@ -41,6 +41,8 @@ struct LevelGeo {
     int xmax;            // first column whose sx+1 >= src width
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
     int chunk0;          // first k_describe block of this level (4 keypoints per block)
+    int64_t blur_off;    // byte offset of the blurred level inside an image's blur workspace
+    int blur_tile0;      // first k_blur tile of this level (64 x 32 tiles)
 };
 
 // One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.
@@ -70,6 +72,8 @@ struct Geo {
     int kp_cap;          // per-image capacity of the final keypoint list (sum of level kp_cap)
     int lvl_kp_cap;      // per-image size of the level-keypoint array (same as kp_cap)
     int64_t ws_bytes;    // per-image pyramid workspace bytes (levels >= 1)
+    int64_t blur_bytes;  // per-image blurred-pyramid bytes (all levels)
+    int blur_tiles;      // k_blur tiles per image
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count
     int max_ncap;        // octree node capacity (max over levels of kp_cap)

@@ -105,6 +105,7 @@ struct orbfe_ctx {
     DevBuf<int> d_chunk_level;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
+    DevBuf<uint8_t> d_blur;
     DevBuf<int> d_cell_count;
     DevBuf<uint32_t> d_slots;
     DevBuf<uint32_t> d_kd;
@@ -248,8 +249,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.yt.clear();
     c.chunk_level.clear();
     c.maxcell = 0;
-    int64_t ws = 0;
-    int kp_off = 0, key_off = 0, chunk = 0;
+    int64_t ws = 0, bws = 0;
+    int kp_off = 0, key_off = 0, chunk = 0, btile = 0;
     int64_t slot_off = 0;
     for (int l = 0; l < L; ++l) {
         LevelGeo& Lg = g.lv[l];
@@ -268,6 +269,10 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
             ws += ((int64_t)Lg.w * Lg.h + 255) & ~(int64_t)255;
             resize_tables(g.lv[l - 1].w, g.lv[l - 1].h, Lg.w, Lg.h, c.prm.resize_simd_lanes, Lg, c.xt, c.yt);
         }
+        Lg.blur_off = bws;
+        bws += ((int64_t)Lg.w * Lg.h + 255) & ~(int64_t)255;
+        Lg.blur_tile0 = btile;
+        btile += ((Lg.w + 63) / 64) * ((Lg.h + 31) / 32);
         Lg.n_feat = c.n_per_level[l];
         Lg.size = (float)(int)(31 * c.sf[l]);
         // cell grid (ORBextractor.cpp:772-806)
@@ -340,6 +345,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.kp_cap = kp_off;
     g.lvl_kp_cap = kp_off;
     g.ws_bytes = std::max<int64_t>(ws, 256);
+    g.blur_bytes = bws;
+    g.blur_tiles = btile;
     g.slot_total = std::max<int64_t>(slot_off, 1);
     g.key_total = std::max(key_off, 1);
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
@@ -371,6 +378,7 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         const Geo& g = c.geo;
         const size_t n = (size_t)max_images;
         c.d_ws.ensure(n * g.ws_bytes);
+        c.d_blur.ensure(n * g.blur_bytes);
         c.d_cell_count.ensure(n * std::max(g.ncells, 1));
         c.d_slots.ensure(n * g.slot_total);
         c.d_kd.ensure(n * g.key_total);
@@ -412,8 +420,9 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     HIPCK(launch_octree(g, c.d_cells.p, c.d_cell_count.p, c.d_slots.p, c.d_kd.p, c.d_kn.p, c.d_lvl_kp.p,
                         c.d_lvl_count.p, c.d_overflow.p, c.maxcell, n, s));
     prof_mark(c, s, 3);
-    HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p, c.d_count.p,
-                          c.d_chunk_level.p, (int)c.chunk_level.size(), n, s));
+    HIPCK(launch_blur(g, d_in, pitch, c.d_ws.p, c.d_blur.p, n, s));
+    HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_blur.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p,
+                          c.d_count.p, c.d_chunk_level.p, (int)c.chunk_level.size(), n, s));
     prof_mark(c, s, 4);
     c.last_in = d_in;
     c.last_pitch = pitch;
@@ -831,9 +840,12 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s));
                     break;
                 case 3:
-                    HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
-                                          h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_chunk_level.p,
-                                          (int)h->chunk_level.size(), n, s));
+                    if (variant != 2)
+                        HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s));
+                    if (variant != 1)
+                        HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
+                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p,
+                                              h->d_chunk_level.p, (int)h->chunk_level.size(), n, s));
                     break;
                 case 4:
                     if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");

@@ -716,21 +716,80 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 }
 
 constexpr int kDescWaves = 4;
-constexpr int kHbStride = kBlurD;  // horizontal-pass rows of 37 columns
 
-// One wavefront per keypoint.  The 43x43 neighbourhood (reflect-101 at the level border, which is
-// where cv::GaussianBlur on the level clone reflects) is staged in LDS once and serves the intensity
-// centroid (radius 15, never reflected), the separable 7x7 blur of the 37x37 sampling disc and the
-// 256 rotated comparisons (assembled by __ballot, 64 bits per round).
+// ------------------------------------------------------------------------------- k_blur
+// cv::GaussianBlur(level clone, 7x7, sigma 2, BORDER_REFLECT_101) for every level of every image, the
+// bit-exact 8U fixed-point path: out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
+// One 256-thread workgroup per 64 x 32 output tile; the (32+6) x (64+6) input (reflect-101 at the
+// level border) is staged in LDS, the horizontal pass is kept as u16 in LDS, the vertical pass
+// writes 4 pixels per thread as one dword when the tile row is aligned.
+constexpr int kBlurTX = 64, kBlurTY = 32;
+
+__global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur) {
+    __shared__ uint8_t src[(kBlurTY + 6) * (kBlurTX + 8)];
+    __shared__ uint16_t hor[(kBlurTY + 6) * kBlurTX];
+    const int img = blockIdx.y, t = threadIdx.x;
+    int l = 0;
+    while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].blur_tile0) ++l;
+    const LevelGeo& L = g.lv[l];
+    const int tile = blockIdx.x - L.blur_tile0;
+    const int ntx = (L.w + kBlurTX - 1) / kBlurTX;
+    const int ty = tile / ntx, tx = tile - ty * ntx;
+    const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
+    int stride;
+    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
+    constexpr int SW = kBlurTX + 6, SP = kBlurTX + 8;
+    for (int i = t; i < (kBlurTY + 6) * SW; i += 256) {
+        const int r = i / SW, c = i - r * SW;
+        src[r * SP + c] = lvl[(int64_t)reflect101(Y0 + r - 3, L.h) * stride + reflect101(X0 + c - 3, L.w)];
+    }
+    __syncthreads();
+    for (int i = t; i < (kBlurTY + 6) * kBlurTX; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const uint8_t* p = src + r * SP + c;
+        hor[i] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3]);
+    }
+    __syncthreads();
+    uint8_t* dst = blur + (int64_t)img * g.blur_bytes + L.blur_off;
+    for (int i = t; i < kBlurTY * (kBlurTX / 4); i += 256) {
+        const int r = i >> 4, c4 = (i & 15) * 4;
+        const int y = Y0 + r;
+        if (y >= L.h) continue;
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint16_t* p = hor + r * kBlurTX + c4 + b;
+            const int v = 18 * (p[0] + p[6 * kBlurTX]) + 34 * (p[kBlurTX] + p[5 * kBlurTX]) +
+                          48 * (p[2 * kBlurTX] + p[4 * kBlurTX]) + 56 * p[3 * kBlurTX];
+            word |= (uint32_t)((v + 32768) >> 16) << (8 * b);
+        }
+        const int x = X0 + c4;
+        uint8_t* o = dst + (int64_t)y * L.w + x;
+        if (x + 3 < L.w && (((uintptr_t)o) & 3) == 0) {
+            *(uint32_t*)o = word;
+        } else {
+            for (int b = 0; b < 4 && x + b < L.w; ++b) o[b] = (uint8_t)(word >> (8 * b));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------- k_describe
+// One wavefront per keypoint, registers only.
+//  IC_Angle (:77-104): the 31 x 31 square around the keypoint is read as 31 rows x 9 aligned dwords
+//  (5 loads per lane, all issued before the first use); each lane accumulates m10 = sum u*I and
+//  m01 = sum v*I over its bytes that fall inside the umax disc; two wave reductions.
+//  computeOrbDescriptor (:108-147): lane j evaluates bits j, j+64, j+128, j+192, i.e. 8 rotated
+//  samples gathered straight from the blurred level (k_blur), assembled by __ballot.
 __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
-                                                  const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
+                                                  const uint8_t* __restrict__ ws, const uint8_t* __restrict__ blur,
+                                                  const uint32_t* __restrict__ lvl_kp,
                                                   const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                   uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                   const int* __restrict__ chunk_level) {
-    __shared__ uint8_t patch[kDescWaves][kPatchD * kPatchD];
-    __shared__ uint16_t hb[kDescWaves][kPatchD * kHbStride];
-    __shared__ uint8_t blur[kDescWaves][kBlurD * kBlurD];
+    __shared__ int s_umax[16];
     const int img = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < 16) s_umax[threadIdx.x] = g.umax[threadIdx.x];
     const int l = chunk_level[blockIdx.x];
     const LevelGeo& L = g.lv[l];
     const int idx = (blockIdx.x - L.chunk0) * kDescWaves + w;
@@ -740,74 +799,69 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
         for (int i = 0; i < g.nlevels; ++i) s += cnt[i];
         out_count[img] = s;
     }
-    const bool active = idx < cnt[l];
+    __syncthreads();
+    if (idx >= cnt[l]) return;  // wave-uniform; no barrier follows
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    int cx = 0, cy = 0, score = 0;
-    if (active) {
-        const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
-        cx = key & 0xFFF;
-        cy = (key >> 12) & 0xFFF;
-        score = key >> 24;
-        for (int i = lane; i < kPatchD * kPatchD; i += 64) {
-            const int r = i / kPatchD - kPatchR, c = i % kPatchD - kPatchR;
-            patch[w][i] = lvl[(int64_t)reflect101(cy + r, L.h) * stride + reflect101(cx + c, L.w)];
+    const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
+    const int cx = key & 0xFFF, cy = (key >> 12) & 0xFFF, score = key >> 24;
+    // ---- intensity centroid
+    uint32_t word[5];
+    int shv[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int slot = lane + 64 * k;
+        word[k] = 0;
+        shv[k] = 0;
+        if (slot < 31 * 9) {
+            const int r = slot / 9, d = slot - r * 9;
+            const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cy - kHalfPatch + r) * stride + cx - kHalfPatch);
+            shv[k] = (int)(a & 3);
+            word[k] = ((const uint32_t*)(a & ~(uintptr_t)3))[d];
         }
     }
-    __syncthreads();
-    float angle = 0.f;
-    if (active) {
-        // intensity centroid over the umax disc (IC_Angle, :77-104): m10 = sum u*I, m01 = sum v*I
-        int m10 = 0, m01 = 0;
-        for (int i = lane; i < 31 * 31; i += 64) {
-            const int v = i / 31 - kHalfPatch, u = i % 31 - kHalfPatch;
-            const int av = v < 0 ? -v : v;
-            if ((u < 0 ? -u : u) <= g.umax[av]) {
-                const int val = patch[w][(kPatchR + v) * kPatchD + kPatchR + u];
-                m10 += u * val;
-                m01 += v * val;
+    int m10 = 0, m01 = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int slot = lane + 64 * k;
+        if (slot < 31 * 9) {
+            const int r = slot / 9, d = slot - r * 9;
+            const int v = r - kHalfPatch, av = v < 0 ? -v : v;
+            const int um = s_umax[av];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * d + b - shv[k] - kHalfPatch;
+                if (u >= -um && u <= um) {
+                    const int val = (word[k] >> (8 * b)) & 0xFF;
+                    m10 += u * val;
+                    m01 += v * val;
+                }
             }
         }
-        m10 = wave_sum(m10);
-        m01 = wave_sum(m01);
-        angle = fast_atan2((float)m01, (float)m10);
-        // horizontal 7-tap pass over 43 rows x 37 columns
-        for (int i = lane; i < kPatchD * kBlurD; i += 64) {
-            const int r = i / kBlurD, c = i % kBlurD;
-            const uint8_t* s = &patch[w][r * kPatchD + c];
-            hb[w][i] = (uint16_t)(18 * s[0] + 34 * s[1] + 48 * s[2] + 56 * s[3] + 48 * s[4] + 34 * s[5] + 18 * s[6]);
-        }
     }
-    __syncthreads();
-    if (active) {
-        for (int i = lane; i < kBlurD * kBlurD; i += 64) {
-            const int r = i / kBlurD, c = i % kBlurD;
-            const uint16_t* s = &hb[w][r * kBlurD + c];
-            const int v = 18 * s[0] + 34 * s[kBlurD] + 48 * s[2 * kBlurD] + 56 * s[3 * kBlurD] + 48 * s[4 * kBlurD] +
-                          34 * s[5 * kBlurD] + 18 * s[6 * kBlurD];
-            blur[w][i] = (uint8_t)((v + 32768) >> 16);
-        }
-    }
-    __syncthreads();
-    if (!active) return;
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // ---- steered BRIEF on the blurred level
     const float factorPI = (float)(M_PI / 180.f);
     float b, a;
     glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
+    const uint8_t* bl = blur + (int64_t)img * g.blur_bytes + L.blur_off + (int64_t)cy * L.w + cx;
+    int val[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int bit = (k >> 1) * 64 + lane;
+        const float px = (float)c_pattern[4 * bit + 2 * (k & 1)], py = (float)c_pattern[4 * bit + 2 * (k & 1) + 1];
+        const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
+        const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
+        val[k] = bl[rr * L.w + cc];
+    }
     int o = idx;
     for (int i = 0; i < l; ++i) o += cnt[i];
     uint64_t* dst = (uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32);
 #pragma unroll
     for (int rnd = 0; rnd < 4; ++rnd) {
-        const int bit = rnd * 64 + lane;
-        int val[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const float px = (float)c_pattern[4 * bit + 2 * k], py = (float)c_pattern[4 * bit + 2 * k + 1];
-            const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
-            const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
-            val[k] = blur[w][(kBlurR + rr) * kBlurD + kBlurR + cc];
-        }
-        const uint64_t m = __ballot(val[0] < val[1]);
+        const uint64_t m = __ballot(val[2 * rnd] < val[2 * rnd + 1]);
         if (lane == 0) dst[rnd] = m;
     }
     if (lane == 0) {
@@ -1064,11 +1118,17 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
     return hipGetLastError();
 }
 
-hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
-                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count,
-                           const int* chunk_level, int n_chunks, int n_images, hipStream_t s) {
-    hipLaunchKernelGGL(k_describe, dim3(n_chunks, n_images), dim3(256), 0, s, g, in, in_pitch, ws, lvl_kp, lvl_count,
-                       out_kp, out_desc, out_count, chunk_level);
+hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* blur, int n_images,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur);
+    return hipGetLastError();
+}
+
+hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
+                           const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
+                           int* out_count, const int* chunk_level, int n_chunks, int n_images, hipStream_t s) {
+    hipLaunchKernelGGL(k_describe, dim3(n_chunks, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur, lvl_kp,
+                       lvl_count, out_kp, out_desc, out_count, chunk_level);
     return hipGetLastError();
 }
 
