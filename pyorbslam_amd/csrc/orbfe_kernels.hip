@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict
     if (t == 0) lvl_count[img * g.nlevels + l] = S;
 }
 
-// ------------------------------------------------------------------------------- k_describe
+// ------------------------------------------------------------------------------- descriptor math
 // glibc 2.35 x86-64 sinf / cosf (FMA ifunc variant; ARM optimized-routines algorithm), |x| < 120.
 struct SinCosTab {
     double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
@@ -720,15 +720,16 @@ constexpr int kDescWaves = 4;
 // ------------------------------------------------------------------------------- k_blur
 // cv::GaussianBlur(level clone, 7x7, sigma 2, BORDER_REFLECT_101) for every level of every image, the
 // bit-exact 8U fixed-point path: out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
-// One 256-thread workgroup per 64 x 32 output tile; the (32+6) x (64+6) input (reflect-101 at the
-// level border) is staged in LDS, the horizontal pass is kept as u16 in LDS, the vertical pass
-// writes 4 pixels per thread as one dword when the tile row is aligned.
-constexpr int kBlurTX = 64, kBlurTY = 32;
+// One 256-thread workgroup per 64 x 32 output tile.  The 70 x 38 input window (column 0 = X0 - 3) is
+// staged in LDS at pitch 80: interior tiles with 19 re-aligned dwords per row (all loads issued before
+// the first wait), border tiles byte by byte through reflect-101.  Each thread then produces 4 adjacent
+// pixels per pass (horizontal into u16 LDS, vertical into one dword store).
+constexpr int kBlurTX = 64, kBlurTY = 32, kBlurSP = 80;
 
 __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                               const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur) {
-    __shared__ uint8_t src[(kBlurTY + 6) * (kBlurTX + 8)];
-    __shared__ uint16_t hor[(kBlurTY + 6) * kBlurTX];
+    __shared__ __attribute__((aligned(16))) uint8_t src[(kBlurTY + 6) * kBlurSP];
+    __shared__ __attribute__((aligned(16))) uint16_t hor[(kBlurTY + 6) * kBlurTX];
     const int img = blockIdx.y, t = threadIdx.x;
     int l = 0;
     while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].blur_tile0) ++l;
@@ -739,33 +740,96 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    constexpr int SW = kBlurTX + 6, SP = kBlurTX + 8;
-    for (int i = t; i < (kBlurTY + 6) * SW; i += 256) {
-        const int r = i / SW, c = i - r * SW;
-        src[r * SP + c] = lvl[(int64_t)reflect101(Y0 + r - 3, L.h) * stride + reflect101(X0 + c - 3, L.w)];
+    // interior: no reflection, and the 19th dword (+1 for re-alignment) stays inside the row band
+    const bool interior = X0 >= 3 && X0 + kBlurTX + 3 + 8 <= L.w && Y0 >= 3 && Y0 + kBlurTY + 3 <= L.h;
+    if (interior) {
+        uint32_t lo[3], hi[3];
+        int sh[3], dst[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {  // 38 rows x 19 dwords = 722 slots, 3 per thread
+            const int slot = t + 256 * k;
+            dst[k] = -1;
+            lo[k] = hi[k] = 0;
+            sh[k] = 0;
+            if (slot < (kBlurTY + 6) * 19) {
+                const int r = slot / 19, d = slot - r * 19;
+                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(Y0 - 3 + r) * stride + X0 - 3);
+                const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
+                sh[k] = (int)(a & 3);
+                lo[k] = p[d];
+                hi[k] = p[d + 1];
+                dst[k] = r * kBlurSP + 4 * d;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (dst[k] >= 0) *(uint32_t*)(src + dst[k]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+    } else {
+        constexpr int SW = kBlurTX + 6;
+        uint8_t v[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int i = t + 256 * k;
+            v[k] = 0;
+            if (i < (kBlurTY + 6) * SW) {
+                const int r = i / SW, c = i - r * SW;
+                v[k] = lvl[(int64_t)reflect101(Y0 + r - 3, L.h) * stride + reflect101(X0 + c - 3, L.w)];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int i = t + 256 * k;
+            if (i < (kBlurTY + 6) * SW) {
+                const int r = i / SW, c = i - r * SW;
+                src[r * kBlurSP + c] = v[k];
+            }
+        }
     }
     __syncthreads();
-    for (int i = t; i < (kBlurTY + 6) * kBlurTX; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        const uint8_t* p = src + r * SP + c;
-        hor[i] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3]);
-    }
-    __syncthreads();
-    uint8_t* dst = blur + (int64_t)img * g.blur_bytes + L.blur_off;
-    for (int i = t; i < kBlurTY * (kBlurTX / 4); i += 256) {
+    // horizontal: 38 rows x 16 groups of 4 columns -> u16
+    for (int i = t; i < (kBlurTY + 6) * 16; i += 256) {
         const int r = i >> 4, c4 = (i & 15) * 4;
-        const int y = Y0 + r;
-        if (y >= L.h) continue;
-        uint32_t word = 0;
+        const uint32_t* p = (const uint32_t*)(src + r * kBlurSP + c4);
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+        int px[10];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const uint16_t* p = hor + r * kBlurTX + c4 + b;
-            const int v = 18 * (p[0] + p[6 * kBlurTX]) + 34 * (p[kBlurTX] + p[5 * kBlurTX]) +
-                          48 * (p[2 * kBlurTX] + p[4 * kBlurTX]) + 56 * p[3 * kBlurTX];
-            word |= (uint32_t)((v + 32768) >> 16) << (8 * b);
+            px[b] = (w0 >> (8 * b)) & 0xFF;
+            px[4 + b] = (w1 >> (8 * b)) & 0xFF;
         }
-        const int x = X0 + c4;
-        uint8_t* o = dst + (int64_t)y * L.w + x;
+        px[8] = w2 & 0xFF;
+        px[9] = (w2 >> 8) & 0xFF;
+        uint32_t o[2];
+#pragma unroll
+        for (int b = 0; b < 4; b += 2) {
+            const uint32_t h0 = 18 * (px[b] + px[b + 6]) + 34 * (px[b + 1] + px[b + 5]) + 48 * (px[b + 2] + px[b + 4]) +
+                                56 * px[b + 3];
+            const uint32_t h1 = 18 * (px[b + 1] + px[b + 7]) + 34 * (px[b + 2] + px[b + 6]) +
+                                48 * (px[b + 3] + px[b + 5]) + 56 * px[b + 4];
+            o[b >> 1] = h0 | (h1 << 16);
+        }
+        *(uint2*)(hor + r * kBlurTX + c4) = make_uint2(o[0], o[1]);
+    }
+    __syncthreads();
+    uint8_t* dstimg = blur + (int64_t)img * g.blur_bytes + L.blur_off;
+    for (int i = t; i < kBlurTY * 16; i += 256) {
+        const int r = i >> 4, c4 = (i & 15) * 4;
+        const int y = Y0 + r, x = X0 + c4;
+        if (y >= L.h || x >= L.w) continue;
+        uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const uint2 q = *(const uint2*)(hor + (r + j) * kBlurTX + c4);
+            const uint32_t kj = j == 3 ? 56 : (j == 2 || j == 4) ? 48 : (j == 1 || j == 5) ? 34 : 18;
+            acc[0] += kj * (q.x & 0xFFFF);
+            acc[1] += kj * (q.x >> 16);
+            acc[2] += kj * (q.y & 0xFFFF);
+            acc[3] += kj * (q.y >> 16);
+        }
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) word |= ((acc[b] + 32768u) >> 16) << (8 * b);
+        uint8_t* o = dstimg + (int64_t)y * L.w + x;
         if (x + 3 < L.w && (((uintptr_t)o) & 3) == 0) {
             *(uint32_t*)o = word;
         } else {
@@ -790,20 +854,25 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     __shared__ int s_umax[16];
     const int img = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x < 16) s_umax[threadIdx.x] = g.umax[threadIdx.x];
-    const int l = chunk_level[blockIdx.x];
+    int l = 0;  // level of this block from the kernel arguments (no table load)
+    while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].chunk0) ++l;
     const LevelGeo& L = g.lv[l];
     const int idx = (blockIdx.x - L.chunk0) * kDescWaves + w;
     const int* cnt = lvl_count + img * g.nlevels;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int s = 0;
-        for (int i = 0; i < g.nlevels; ++i) s += cnt[i];
-        out_count[img] = s;
+    // the packed key can be read before knowing whether idx < count (the slot always exists)
+    const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
+    int o = idx, n_l = 0, total = 0;
+    for (int i = 0; i < g.nlevels; ++i) {
+        const int ci = cnt[i];
+        o += i < l ? ci : 0;
+        n_l = i == l ? ci : n_l;
+        total += ci;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out_count[img] = total;
     __syncthreads();
-    if (idx >= cnt[l]) return;  // wave-uniform; no barrier follows
+    if (idx >= n_l) return;  // wave-uniform; no barrier follows
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
     const int cx = key & 0xFFF, cy = (key >> 12) & 0xFFF, score = key >> 24;
     // ---- intensity centroid
     uint32_t word[5];
@@ -856,8 +925,6 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
         const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
         val[k] = bl[rr * L.w + cc];
     }
-    int o = idx;
-    for (int i = 0; i < l; ++i) o += cnt[i];
     uint64_t* dst = (uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32);
 #pragma unroll
     for (int rnd = 0; rnd < 4; ++rnd) {
