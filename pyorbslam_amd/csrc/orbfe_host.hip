@@ -119,6 +119,10 @@ struct orbfe_ctx {
     DevBuf<float> d_uR, d_depth;
     DevBuf<int8_t> d_status;
     DevBuf<int32_t> d_match;
+    DevBuf<int> d_boff;
+    DevBuf<uint16_t> d_bidx;
+    DevBuf<float2> d_rinfo;
+    int64_t bucket_cap = 0;
     // hamming scratch
     DevBuf<uint8_t> d_hq, d_ht;
     DevBuf<int> d_hoff, d_hidx, d_hres;
@@ -394,6 +398,11 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.d_depth.ensure(np * g.kp_cap);
         c.d_status.ensure(np * g.kp_cap);
         c.d_match.ensure(np * g.kp_cap);
+        // a right keypoint covers at most ceil(y+2s) - floor(y-2s) + 1 <= 4 s_max + 3 rows
+        c.bucket_cap = (int64_t)g.kp_cap * (int64_t)(4 * c.sf[g.nlevels - 1] + 4);
+        c.d_boff.ensure(np * (g.H + 1));
+        c.d_bidx.ensure(np * c.bucket_cap);
+        c.d_rinfo.ensure(np * g.kp_cap);
         c.max_images = max_images;
     }
 }
@@ -430,6 +439,13 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     c.last_stream = s;
 }
 
+void stereo_buffers(orbfe_ctx& c, StereoArgs& a) {
+    a.bucket_off = c.d_boff.p;
+    a.bucket_idx = c.d_bidx.p;
+    a.bucket_cap = c.bucket_cap;
+    a.rinfo = c.d_rinfo.p;
+}
+
 void stereo_consts(double bf, float fx, StereoArgs& a) {
     const float bf32 = (float)bf;                 // NEP 50: the Python float meets an np.float32
     const float mb = bf32 / fx;                   // Frame.py:43  mbf / mK[0][0]
@@ -462,6 +478,7 @@ void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStr
     a.status = c.d_status.p;
     a.match_r = c.d_match.p;
     a.out_stride = g.kp_cap;
+    stereo_buffers(c, a);
     stereo_consts(bf, fx, a);
     c.last_bf = bf;
     c.last_fx = fx;
@@ -611,6 +628,8 @@ int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, fl
         a.status = hl->d_status.p;
         a.match_r = hl->d_match.p;
         a.out_stride = g.kp_cap;
+        stereo_buffers(*hl, a);
+        a.kp_stride = 0;
         stereo_consts(bf, fx, a);
         hipStream_t s = own(*hl);
         HIPCK(launch_stereo(g, a, 1, s));

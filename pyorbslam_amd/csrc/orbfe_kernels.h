@@ -29,6 +29,12 @@ struct StereoArgs {
     int8_t* status;
     int32_t* match_r;
     int64_t out_stride;
+    // row buckets (k_stereo_bucket): per pair (H + 1) offsets and bucket_cap right-keypoint indices,
+    // plus out_stride compact (x, octave-as-bits) records per pair
+    int* bucket_off;
+    uint16_t* bucket_idx;
+    int64_t bucket_cap;
+    float2* rinfo;
     float maxD;               // np.float32(bf / np.float32(bf / fx32))   (Frame.py:43, 181-183)
     float bf32;               // np.float32(bf): what `mbf / disparity` promotes bf to
     double bf;

@@ -954,45 +954,94 @@ __device__ __forceinline__ int sheared_px(const uint8_t* lvl, int stride, int w,
 
 __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Python round(): half to even
 
+// Row buckets of the right keypoints (Frame.py:170-179): right keypoint iR is listed in every row of
+// [floor(y - 2s), ceil(y + 2s)] (double arithmetic, s = scale of its octave).  One workgroup per pair:
+// LDS histogram -> block scan -> fill.  The order inside a bucket is irrelevant: k_stereo reduces
+// (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
+// Also writes the compact (x, octave) record of every right keypoint.
+__global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
+    extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
+    __shared__ int scan_tmp[257];
+    const int pr = blockIdx.x, t = threadIdx.x;
+    const int H = g.H, nR = A.countR[pr * A.cnt_stride];
+    const orbfe_keypoint* KR = A.kpsR + pr * A.kp_stride;
+    int* off = A.bucket_off + (int64_t)pr * (H + 1);
+    uint16_t* idx = A.bucket_idx + (int64_t)pr * A.bucket_cap;
+    float2* rinfo = A.rinfo + pr * A.out_stride;
+    for (int i = t; i <= H; i += 256) cnt[i] = 0;
+    __syncthreads();
+    for (int i = t; i < nR; i += 256) {
+        const orbfe_keypoint kr = KR[i];
+        rinfo[i] = make_float2(kr.x, __int_as_float(kr.octave));
+        const double r = 2.0 * (double)g.scale[kr.octave];
+        const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
+        for (int y = lo; y <= hi; ++y) atomicAdd(&cnt[y], 1);
+    }
+    __syncthreads();
+    const int total = block_excl_scan(cnt, H, scan_tmp);
+    if (t == 0) cnt[H] = total;
+    __syncthreads();
+    for (int i = t; i <= H; i += 256) off[i] = cnt[i];
+    __syncthreads();
+    for (int i = t; i < nR; i += 256) {
+        const orbfe_keypoint kr = KR[i];
+        const double r = 2.0 * (double)g.scale[kr.octave];
+        const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
+        for (int y = lo; y <= hi; ++y) {
+            const int pos = atomicAdd(&cnt[y], 1);
+            if (pos < A.bucket_cap) idx[pos] = (uint16_t)i;
+        }
+    }
+}
+
+// One wavefront per left keypoint (Frame.py:186-278).
+//  search: the row bucket of int(vL); gates |octR - octL| <= 1 and uL - maxD <= uR <= uL; Hamming
+//          distance by 8 popcounts; (distance, iR) lexicographic wave minimum; accept if < 75
+//          (TH_HIGH start 100, thOrbDist = (TH_HIGH + TH_LOW) / 2).
+//  refine: the 11 x 11 left patch and the 11 x 21 right strip of the *sheared* pyramid views are
+//          staged in LDS (one index division per staged pixel), 11 shifts x 11 rows of SAD sums, first
+//          minimum, parabola and depth in IEEE float32 like the NumPy-2 chain of the reference.
 __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     __shared__ int sad[4][11];
+    __shared__ uint8_t sL[4][121];
+    __shared__ uint8_t sR[4][231];
     const int pr = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int iL = blockIdx.x * 4 + w;
-    const int nL = A.countL[pr * A.cnt_stride], nR = A.countR[pr * A.cnt_stride];
+    const int nL = A.countL[pr * A.cnt_stride];
     const bool active = iL < nL;
     const orbfe_keypoint* KL = A.kpsL + pr * A.kp_stride;
     const orbfe_keypoint* KR = A.kpsR + pr * A.kp_stride;
     const uint8_t* DL = A.descL + pr * A.kp_stride * 32;
     const uint8_t* DR = A.descR + pr * A.kp_stride * 32;
+    const float2* rinfo = A.rinfo + pr * A.out_stride;
     if (lane < 11) sad[w][lane] = 0;
     int best = 256, bidx = 0x7fffffff;
     orbfe_keypoint kl;
     if (active) {
         kl = KL[iL];
-        const int row = (int)(double)kl.y;
+        const int row = min((int)(double)kl.y, g.H - 1);
+        const int* off = A.bucket_off + (int64_t)pr * (g.H + 1);
+        const uint16_t* bidxs = A.bucket_idx + (int64_t)pr * A.bucket_cap;
+        const int b = off[row], e = min(off[row + 1], A.bucket_cap);
         const float minU = __fsub_rn(kl.x, A.maxD);
         const uint4* dl4 = (const uint4*)(DL + (int64_t)iL * 32);
         const uint4 a0 = dl4[0], a1 = dl4[1];
-        for (int c0 = 0; c0 < nR; c0 += 64) {
-            const int iR = c0 + lane;
-            if (iR >= nR) break;
-            const orbfe_keypoint kr = KR[iR];
-            const double r = 2.0 * (double)g.scale[kr.octave];
-            const double maxr = ceil((double)kr.y + r), minr = floor((double)kr.y - r);
-            if (!(minr <= row && row <= maxr)) continue;
-            if (kr.octave < kl.octave - 1 || kr.octave > kl.octave + 1) continue;
-            if (!(minU <= kr.x && (double)kr.x <= (double)kl.x)) continue;
+        for (int k = b + lane; k < e; k += 64) {
+            const int iR = bidxs[k];
+            const float2 ri = rinfo[iR];
+            const int oct = __float_as_int(ri.y);
+            if (oct < kl.octave - 1 || oct > kl.octave + 1) continue;
+            if (!(minU <= ri.x && (double)ri.x <= (double)kl.x)) continue;
             const uint4* dr4 = (const uint4*)(DR + (int64_t)iR * 32);
             const uint4 b0 = dr4[0], b1 = dr4[1];
             const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
                              __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-            if (dist < best) {  // per-lane first minimum (lane's iR increase)
+            if (dist < best || (dist == best && iR < bidx)) {
                 best = dist;
                 bidx = iR;
             }
         }
     }
-    // wave argmin on (dist, iR): the reference keeps the first strict minimum in ascending iR
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bidx, o, 64);
@@ -1001,11 +1050,10 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             bidx = oi;
         }
     }
-    __syncthreads();
     int status = 0;
     float uR = -1.f, depth = -1.f;
-    const bool refine = active && best < 100 && best < 75;  // TH_HIGH start, thOrbDist = 75 (:166, :203, :222)
-    int scaleduR0 = 0, scaledvL = 0, scaleduL = 0, lw = 0, lh = 0, lstride = 0, rstride = 0;
+    const bool refine = active && best < 75;  // TH_HIGH start, thOrbDist = 75 (:166, :203, :222)
+    int scaleduR0 = 0, scaledvL = 0, scaleduL = 0, lw = 0, lh = 0, lstride = 0;
     const uint8_t *lvlL = nullptr, *lvlR = nullptr;
     bool do_sad = false;
     if (refine) {
@@ -1020,28 +1068,37 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         if (oct == 0) {
             lvlL = A.lvl0L + pr * A.lvl0_stride;
             lvlR = A.lvl0R + pr * A.lvl0_stride;
-            lstride = rstride = g.W;
+            lstride = g.W;
         } else {
             lvlL = A.wsL + pr * A.ws_stride + g.lv[oct].ws_off;
             lvlR = A.wsR + pr * A.ws_stride + g.lv[oct].ws_off;
-            lstride = rstride = lw;
+            lstride = lw;
         }
-        // iniu < 0 or endu >= cols (:240-243); slices stay inside the level otherwise
+        // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
                  scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
+        if (do_sad) {
+            for (int i = lane; i < 121; i += 64) {
+                const int r = i / 11, c = i - r * 11;
+                sL[w][i] = (uint8_t)sheared_px(lvlL, lstride, lw, lh, scaledvL - 5 + r, scaleduL - 5 + c);
+            }
+            for (int i = lane; i < 231; i += 64) {
+                const int r = i / 21, c = i - r * 21;
+                sR[w][i] = (uint8_t)sheared_px(lvlR, lstride, lw, lh, scaledvL - 5 + r, scaleduR0 - 10 + c);
+            }
+        }
     }
+    __syncthreads();
     if (do_sad) {
-        const int lc = sheared_px(lvlL, lstride, lw, lh, scaledvL, scaleduL);
+        const int lc = sL[w][60];  // IL[5][5]
         // 11 shifts x 11 rows = 121 row sums of 11 |(IL - IL[5,5]) - (IR - IR[5,5])| terms
         for (int it = lane; it < 121; it += 64) {
-            const int s = it / 11, r = it % 11, inc = s - 5;
-            const int yy = scaledvL - 5 + r;
-            const int rc = sheared_px(lvlR, rstride, lw, lh, scaledvL, scaleduR0 + inc);
+            const int s = it / 11, r = it - s * 11;
+            const int rc = sR[w][5 * 21 + s + 5];
             int acc = 0;
+#pragma unroll
             for (int c = 0; c < 11; ++c) {
-                const int il = sheared_px(lvlL, lstride, lw, lh, yy, scaleduL - 5 + c) - lc;
-                const int ir = sheared_px(lvlR, rstride, lw, lh, yy, scaleduR0 + inc - 5 + c) - rc;
-                const int dd = il - ir;
+                const int dd = (sL[w][r * 11 + c] - lc) - (sR[w][r * 21 + s + c] - rc);
                 acc += dd < 0 ? -dd : dd;
             }
             atomicAdd(&sad[w][s], acc);
@@ -1200,6 +1257,7 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
 }
 
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
+    hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);
     hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 3) / 4, n_pairs), dim3(256), 0, s, g, a);
     return hipGetLastError();
 }
