@@ -23,6 +23,7 @@ constexpr int kMaxCellRoi = 64;    // max cell ROI side (wCell+6, hCell+6); chec
 // One pyramid level of one image geometry.
 struct LevelGeo {
     int w, h;            // level size: cvRound(W * invScale), cvRound(H * invScale) (:1110-1111)
+    int pitch;           // row pitch of the level in the pyramid / blur workspaces (w rounded up to 16)
     int64_t ws_off;      // byte offset of the level inside an image's pyramid workspace (levels >= 1)
     float scale, inv_scale;
     int n_feat;          // mnFeaturesPerLevel[l]

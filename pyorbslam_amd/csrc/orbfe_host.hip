@@ -199,6 +199,7 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
     const bool area_fast = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON;
     if (area_fast && isx == 2 && isy == 2)
         throw Error(ORBFE_EINVAL, "scale factor 2 selects cv::resize's INTER_AREA path, which is not implemented");
+    while (xt.size() % 4) xt.push_back(ResizeX{0, 0, 0});  // k_resize reads 4 entries as 2 x 16 bytes
     Lg.xtab_off = (int)xt.size();
     Lg.ytab_off = (int)yt.size();
     int xmax = dw;
@@ -218,6 +219,7 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
         xt.push_back(r);
     }
     Lg.xmax = xmax;
+    for (int k = 0; k < 4; ++k) xt.push_back(ResizeX{0, 0, 0});  // over-read guard of the last group
     int xv = 0;
     if (simd > 0) {
         while (xv <= dw - simd) xv += simd;
@@ -268,13 +270,14 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
             throw Error(ORBFE_EINVAL, "level size out of range (1..4095 px per side)");
         if (Lg.w <= kEdge || Lg.h <= kEdge)
             throw Error(ORBFE_EINVAL, "image too small: a pyramid level is not wider than the 19 px reflect border");
+        Lg.pitch = (Lg.w + 15) & ~15;
         if (l > 0) {
             Lg.ws_off = ws;
-            ws += ((int64_t)Lg.w * Lg.h + 255) & ~(int64_t)255;
+            ws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
             resize_tables(g.lv[l - 1].w, g.lv[l - 1].h, Lg.w, Lg.h, c.prm.resize_simd_lanes, Lg, c.xt, c.yt);
         }
         Lg.blur_off = bws;
-        bws += ((int64_t)Lg.w * Lg.h + 255) & ~(int64_t)255;
+        bws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
         Lg.blur_tile0 = btile;
         btile += ((Lg.w + 63) / 64) * ((Lg.h + 31) / 32);
         Lg.n_feat = c.n_per_level[l];
@@ -585,7 +588,8 @@ int orbfe_pyramid(orbfe_handle h, int32_t level, uint8_t* out, int32_t sheared, 
         if (!out) return;
         std::vector<uint8_t> lv((size_t)L.w * L.h);
         const uint8_t* src = level == 0 ? h->d_in.p : h->d_ws.p + L.ws_off;
-        HIPCK(hipMemcpy(lv.data(), src, lv.size(), hipMemcpyDeviceToHost));
+        const size_t spitch = level == 0 ? (size_t)L.w : (size_t)L.pitch;
+        HIPCK(hipMemcpy2D(lv.data(), L.w, src, spitch, L.w, L.h, hipMemcpyDeviceToHost));
         if (!sheared) {
             std::memcpy(out, lv.data(), lv.size());
             return;

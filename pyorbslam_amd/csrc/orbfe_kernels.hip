@@ -42,7 +42,7 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const u
         *stride = g.W;
         return in + (int64_t)img * in_pitch;
     }
-    *stride = g.lv[l].w;
+    *stride = g.lv[l].pitch;
     return ws + (int64_t)img * g.ws_bytes + g.lv[l].ws_off;
 }
 
@@ -96,36 +96,89 @@ __device__ int block_sum(int v, int* red) {
 }
 
 // ------------------------------------------------------------------------------- k_resize
-// One thread per output pixel of level l (l >= 1), source = unpadded level l-1.
+// 4 output pixels per thread of level l (l >= 1) from the unpadded level l-1: the 4 column
+// coefficients come in as two 16-byte loads, each source row as 3 aligned dwords (the 4 columns span
+// at most 6 source bytes at the pyramid's scale factors; a byte path covers wider spans and the right
+// edge), and the 4 results leave as one aligned dword (level rows are padded to a 16-byte pitch).
+__device__ __forceinline__ int pick_byte(uint32_t w0, uint32_t w1, uint32_t w2, int o) {
+    const uint32_t w = o < 4 ? w0 : (o < 8 ? w1 : w2);
+    return (w >> (8 * (o & 3))) & 0xFF;
+}
+
 __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                 uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
     const LevelGeo& L = g.lv[l];
+    const LevelGeo& P = g.lv[l - 1];
     const int img = blockIdx.z, dy = blockIdx.y;
-    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dx = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
     if (dx >= L.w) return;
     int sstride;
     const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
     const ResizeY ry = yt[L.ytab_off + dy];
-    const ResizeX rx = xt[L.xtab_off + dx];
-    const uint8_t* r0 = src + (int64_t)ry.sy0 * sstride + rx.sx;
-    const uint8_t* r1 = src + (int64_t)ry.sy1 * sstride + rx.sx;
-    int h0, h1;
-    if (dx < L.xmax) {
-        h0 = r0[0] * rx.a0 + r0[1] * rx.a1;
-        h1 = r1[0] * rx.a0 + r1[1] * rx.a1;
+    ResizeX e[4];
+    {
+        const uint4* xp = (const uint4*)(xt + L.xtab_off + dx);  // xtab_off is a multiple of 4
+        const uint4 q0 = xp[0], q1 = xp[1];
+        e[0].sx = (int)q0.x; e[0].a0 = (int16_t)(q0.y & 0xFFFF); e[0].a1 = (int16_t)(q0.y >> 16);
+        e[1].sx = (int)q0.z; e[1].a0 = (int16_t)(q0.w & 0xFFFF); e[1].a1 = (int16_t)(q0.w >> 16);
+        e[2].sx = (int)q1.x; e[2].a0 = (int16_t)(q1.y & 0xFFFF); e[2].a1 = (int16_t)(q1.y >> 16);
+        e[3].sx = (int)q1.z; e[3].a0 = (int16_t)(q1.w & 0xFFFF); e[3].a1 = (int16_t)(q1.w >> 16);
+    }
+    const uint8_t* r0 = src + (int64_t)ry.sy0 * sstride;
+    const uint8_t* r1 = src + (int64_t)ry.sy1 * sstride;
+    const int last = min(dx + 3, L.w - 1) - dx;  // valid columns 0..last
+    const int sxa = e[0].sx & ~3;
+    const bool fast = e[last].sx + 1 - sxa < 12 && sxa + 16 <= P.w;  // 4th dword stays in the row
+    int h0[4], h1[4];
+    if (fast) {
+        const uint32_t* p0 = (const uint32_t*)(((uintptr_t)(r0 + sxa)) & ~(uintptr_t)3);
+        const uint32_t* p1 = (const uint32_t*)(((uintptr_t)(r1 + sxa)) & ~(uintptr_t)3);
+        const int s0 = (int)(((uintptr_t)(r0 + sxa)) & 3), s1 = (int)(((uintptr_t)(r1 + sxa)) & 3);
+        const uint32_t a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+        const uint32_t b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+        // re-align both 12-byte windows so byte o is source column sxa + o
+        const uint32_t u0 = __builtin_amdgcn_alignbyte(a1, a0, s0), u1 = __builtin_amdgcn_alignbyte(a2, a1, s0),
+                       u2 = __builtin_amdgcn_alignbyte(a3, a2, s0);
+        const uint32_t v0 = __builtin_amdgcn_alignbyte(b1, b0, s1), v1 = __builtin_amdgcn_alignbyte(b2, b1, s1),
+                       v2 = __builtin_amdgcn_alignbyte(b3, b2, s1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int o = e[k].sx - sxa;
+            if (dx + k < L.xmax) {
+                h0[k] = pick_byte(u0, u1, u2, o) * e[k].a0 + pick_byte(u0, u1, u2, o + 1) * e[k].a1;
+                h1[k] = pick_byte(v0, v1, v2, o) * e[k].a0 + pick_byte(v0, v1, v2, o + 1) * e[k].a1;
+            } else {
+                h0[k] = pick_byte(u0, u1, u2, o) * 2048;
+                h1[k] = pick_byte(v0, v1, v2, o) * 2048;
+            }
+        }
     } else {
-        h0 = r0[0] * 2048;
-        h1 = r1[0] * 2048;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sx = e[k > last ? last : k].sx;
+            if (dx + k < L.xmax) {
+                h0[k] = r0[sx] * e[k].a0 + r0[sx + 1] * e[k].a1;
+                h1[k] = r1[sx] * e[k].a0 + r1[sx + 1] * e[k].a1;
+            } else {
+                h0[k] = r0[sx] * 2048;
+                h1[k] = r1[sx] * 2048;
+            }
+        }
     }
-    int v;
-    if (dx < L.xvec) {  // OpenCV VResizeLinearVec_32s8u: v_mul_hi on (S>>4) packed to int16, then (x+2)>>2
-        const int a0 = min(h0 >> 4, 32767), a1 = min(h1 >> 4, 32767);
-        v = (((a0 * ry.b0) >> 16) + ((a1 * ry.b1) >> 16) + 2) >> 2;
-    } else {            // FixedPtCast<int, uchar, 22>
-        v = (h0 * ry.b0 + h1 * ry.b1 + (1 << 21)) >> 22;
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int v;
+        if (dx + k < L.xvec) {  // OpenCV VResizeLinearVec_32s8u: v_mul_hi on (S>>4) packed to int16, (x+2)>>2
+            const int a0 = min(h0[k] >> 4, 32767), a1 = min(h1[k] >> 4, 32767);
+            v = (((a0 * ry.b0) >> 16) + ((a1 * ry.b1) >> 16) + 2) >> 2;
+        } else {                // FixedPtCast<int, uchar, 22>
+            v = (h0[k] * ry.b0 + h1[k] * ry.b1 + (1 << 21)) >> 22;
+        }
+        word |= (uint32_t)min(max(v, 0), 255) << (8 * k);
     }
-    ws[(int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy * L.w + dx] = (uint8_t)min(max(v, 0), 255);
+    *(uint32_t*)(ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy * L.pitch + dx) = word;
 }
 
 // ------------------------------------------------------------------------------- k_detect
@@ -829,12 +882,8 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
         uint32_t word = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) word |= ((acc[b] + 32768u) >> 16) << (8 * b);
-        uint8_t* o = dstimg + (int64_t)y * L.w + x;
-        if (x + 3 < L.w && (((uintptr_t)o) & 3) == 0) {
-            *(uint32_t*)o = word;
-        } else {
-            for (int b = 0; b < 4 && x + b < L.w; ++b) o[b] = (uint8_t)(word >> (8 * b));
-        }
+        // rows are padded to a 16-byte pitch, so the dword never leaves the row's allocation
+        *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = word;
     }
 }
 
@@ -915,7 +964,7 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     const float factorPI = (float)(M_PI / 180.f);
     float b, a;
     glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
-    const uint8_t* bl = blur + (int64_t)img * g.blur_bytes + L.blur_off + (int64_t)cy * L.w + cx;
+    const uint8_t* bl = blur + (int64_t)img * g.blur_bytes + L.blur_off + (int64_t)cy * L.pitch + cx;
     int val[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -923,7 +972,7 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
         const float px = (float)c_pattern[4 * bit + 2 * (k & 1)], py = (float)c_pattern[4 * bit + 2 * (k & 1) + 1];
         const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
         const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
-        val[k] = bl[rr * L.w + cc];
+        val[k] = bl[rr * L.pitch + cc];
     }
     uint64_t* dst = (uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32);
 #pragma unroll
@@ -1072,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         } else {
             lvlL = A.wsL + pr * A.ws_stride + g.lv[oct].ws_off;
             lvlR = A.wsR + pr * A.ws_stride + g.lv[oct].ws_off;
-            lstride = lw;
+            lstride = g.lv[oct].pitch;
         }
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
@@ -1208,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restric
 // ------------------------------------------------------------------------------- launchers
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s) {
-    dim3 grid((g.lv[l].w + 255) / 256, g.lv[l].h, n_images);
+    dim3 grid((g.lv[l].w + 1023) / 1024, g.lv[l].h, n_images);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();
 }
