@@ -78,6 +78,9 @@ struct Geo {
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count
     int max_ncap;        // octree node capacity (max over levels of kp_cap)
+    int rs_nsrc;         // k_resize: most source rows one 8-row output band needs
+    int rs_sp;           // k_resize: largest source row stride (W for the input, pitch for derived levels)
+    int rs_ngrp;         // k_resize: most 4-pixel groups in a derived level row (multiple of 4)
     int max_rh;          // largest FAST cell ROI height (rows)
     int max_wh;          // largest FAST detection window height (rows)
     int max_win;         // largest FAST detection window (pixels), rounded up to 16

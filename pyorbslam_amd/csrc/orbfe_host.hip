@@ -219,7 +219,13 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
         xt.push_back(r);
     }
     Lg.xmax = xmax;
-    for (int k = 0; k < 4; ++k) xt.push_back(ResizeX{0, 0, 0});  // over-read guard of the last group
+    // over-read guard of the last group: the last column at weight 2048 (kept inside its group's byte window)
+    for (int k = 0; k < 4; ++k) xt.push_back(ResizeX{sw - 1, 2048, 0});
+    // k_resize gathers a 4-pixel group's taps from 8 bytes starting at the group's first sx
+    for (int g0 = Lg.xtab_off; g0 < (int)xt.size() - 4; g0 += 4)
+        for (int k = 1; k < 4; ++k)
+            if (xt[g0 + k].sx - xt[g0].sx < 0 || xt[g0 + k].sx - xt[g0].sx > 6)
+                throw Error(ORBFE_EINVAL, "resize step too large for k_resize's 8-byte tap window");
     int xv = 0;
     if (simd > 0) {
         while (xv <= dw - simd) xv += simd;
@@ -351,6 +357,21 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.ncells = (int)c.cells.size();
     g.kp_cap = kp_off;
     g.lvl_kp_cap = kp_off;
+    // k_resize geometry: source rows per 8-row output band, source row stride, groups per row
+    g.rs_nsrc = 1;
+    g.rs_sp = g.W;
+    g.rs_ngrp = 4;
+    for (int l = 1; l < L; ++l) {
+        const LevelGeo& Lg = g.lv[l];
+        for (int dy0 = 0; dy0 < Lg.h; dy0 += 8) {
+            const int dy1 = std::min(dy0 + 8, Lg.h);
+            g.rs_nsrc = std::max(g.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
+        }
+        if (l >= 2) g.rs_sp = std::max(g.rs_sp, g.lv[l - 1].pitch);
+        g.rs_ngrp = std::max(g.rs_ngrp, ((Lg.w + 3) / 4 + 3) & ~3);
+    }
+    if ((int64_t)g.rs_ngrp * 36 + 128 + (int64_t)g.rs_nsrc * g.rs_sp + 16 > 150 * 1024)
+        throw Error(ORBFE_EINVAL, "image too wide for the k_resize band staging (LDS)");
     g.ws_bytes = std::max<int64_t>(ws, 256);
     g.blur_bytes = bws;
     g.blur_tiles = btile;
@@ -852,7 +873,7 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
             switch (stage) {
                 case 0:
                     for (int l = 1; l < g.nlevels; ++l)
-                        HIPCK(launch_resize(g, l, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, n, s));
+                        HIPCK(launch_resize(g, l, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, n, s, variant));
                     break;
                 case 1:
                     HIPCK(launch_detect(g, h->d_cells.p, h->last_in, h->last_pitch, h->d_ws.p, h->d_cell_count.p,

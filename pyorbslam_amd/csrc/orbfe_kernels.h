@@ -41,7 +41,7 @@ struct StereoArgs {
 };
 
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
-                         const ResizeY* yt, int n_images, hipStream_t s);
+                         const ResizeY* yt, int n_images, hipStream_t s, int variant = 0);
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant = 0);
 size_t octree_lds_bytes(const Geo& g, int maxcell);

@@ -96,89 +96,120 @@ __device__ int block_sum(int v, int* red) {
 }
 
 // ------------------------------------------------------------------------------- k_resize
-// 4 output pixels per thread of level l (l >= 1) from the unpadded level l-1: the 4 column
-// coefficients come in as two 16-byte loads, each source row as 3 aligned dwords (the 4 columns span
-// at most 6 source bytes at the pyramid's scale factors; a byte path covers wider spans and the right
-// edge), and the 4 results leave as one aligned dword (level rows are padded to a 16-byte pitch).
-__device__ __forceinline__ int pick_byte(uint32_t w0, uint32_t w1, uint32_t w2, int o) {
-    const uint32_t w = o < 4 ? w0 : (o < 8 ? w1 : w2);
-    return (w >> (8 * (o & 3))) & 0xFF;
-}
+// One 256-thread workgroup per band of kRsRows output rows of level l (l >= 1), full width.
+//  * staging: the source rows the band reads (sy0(first) .. sy1(last) of level l-1) are one contiguous
+//    byte range in memory for every level (stride W for the input, the 16-byte pitch for derived levels),
+//    so they are copied to LDS as a flat run of aligned dwords, every load issued before the first wait;
+//    LDS byte sh0 + r * stride + c holds source row ys_lo + r, column c (sh0 = the range's misalignment).
+//  * the level's x coefficients become, per 4-pixel group, v_perm selectors into an 8-byte tap window
+//    starting at the group's first sx plus the packed (a0, a1) weights, stored once per block as SoA.
+//  * compute: per group and row, 2 x (3 LDS dwords, 2 v_alignbyte, 4 v_perm + 4 v_dot2_u32_u16) for the
+//    horizontal taps, then OpenCV's vertical rounding; one aligned dword store per 4 output pixels.
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+constexpr int kRsRows = 8;
+constexpr int kRsSlots = 16;  // staged dwords per thread per pass
 
+template <int V>  // V: 0 full kernel; ablations for tools/microbench.py: 1 staging only, 2 compute only
 __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                 uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
+    uint4* s_sel = (uint4*)rs_lds;                       // g.rs_ngrp groups each
+    uint4* s_aa = s_sel + g.rs_ngrp;
+    int* s_sx0 = (int*)(s_aa + g.rs_ngrp);
+    uint32_t* s_ry = (uint32_t*)(s_sx0 + g.rs_ngrp);     // kRsRows ResizeY as 3 dwords
+    uint32_t* s_src = s_ry + 4 * kRsRows;                // staged source rows
     const LevelGeo& L = g.lv[l];
     const LevelGeo& P = g.lv[l - 1];
-    const int img = blockIdx.z, dy = blockIdx.y;
-    const int dx = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-    if (dx >= L.w) return;
+    const int img = blockIdx.y, t = threadIdx.x;
+    const int dy0 = blockIdx.x * kRsRows, nrow = min(kRsRows, L.h - dy0);
+    const int ngrp = (L.w + 3) >> 2;
     int sstride;
     const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
-    const ResizeY ry = yt[L.ytab_off + dy];
-    ResizeX e[4];
-    {
-        const uint4* xp = (const uint4*)(xt + L.xtab_off + dx);  // xtab_off is a multiple of 4
-        const uint4 q0 = xp[0], q1 = xp[1];
-        e[0].sx = (int)q0.x; e[0].a0 = (int16_t)(q0.y & 0xFFFF); e[0].a1 = (int16_t)(q0.y >> 16);
-        e[1].sx = (int)q0.z; e[1].a0 = (int16_t)(q0.w & 0xFFFF); e[1].a1 = (int16_t)(q0.w >> 16);
-        e[2].sx = (int)q1.x; e[2].a0 = (int16_t)(q1.y & 0xFFFF); e[2].a1 = (int16_t)(q1.y >> 16);
-        e[3].sx = (int)q1.z; e[3].a0 = (int16_t)(q1.w & 0xFFFF); e[3].a1 = (int16_t)(q1.w >> 16);
-    }
-    const uint8_t* r0 = src + (int64_t)ry.sy0 * sstride;
-    const uint8_t* r1 = src + (int64_t)ry.sy1 * sstride;
-    const int last = min(dx + 3, L.w - 1) - dx;  // valid columns 0..last
-    const int sxa = e[0].sx & ~3;
-    const bool fast = e[last].sx + 1 - sxa < 12 && sxa + 16 <= P.w;  // 4th dword stays in the row
-    int h0[4], h1[4];
-    if (fast) {
-        const uint32_t* p0 = (const uint32_t*)(((uintptr_t)(r0 + sxa)) & ~(uintptr_t)3);
-        const uint32_t* p1 = (const uint32_t*)(((uintptr_t)(r1 + sxa)) & ~(uintptr_t)3);
-        const int s0 = (int)(((uintptr_t)(r0 + sxa)) & 3), s1 = (int)(((uintptr_t)(r1 + sxa)) & 3);
-        const uint32_t a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-        const uint32_t b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
-        // re-align both 12-byte windows so byte o is source column sxa + o
-        const uint32_t u0 = __builtin_amdgcn_alignbyte(a1, a0, s0), u1 = __builtin_amdgcn_alignbyte(a2, a1, s0),
-                       u2 = __builtin_amdgcn_alignbyte(a3, a2, s0);
-        const uint32_t v0 = __builtin_amdgcn_alignbyte(b1, b0, s1), v1 = __builtin_amdgcn_alignbyte(b2, b1, s1),
-                       v2 = __builtin_amdgcn_alignbyte(b3, b2, s1);
+    const int ys_lo = yt[L.ytab_off + dy0].sy0, ys_hi = yt[L.ytab_off + dy0 + nrow - 1].sy1;
+    const uintptr_t a0 = (uintptr_t)(src + (int64_t)ys_lo * sstride);
+    const int sh0 = (int)(a0 & 3);
+    const uint32_t* gsrc = (const uint32_t*)(a0 - sh0);
+    const int ndw = ((ys_hi - ys_lo) * sstride + P.w + sh0 + 3) >> 2;
+    for (int base = 0; base < (V == 2 ? 0 : ndw); base += 256 * kRsSlots) {
+        uint32_t v[kRsSlots];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int o = e[k].sx - sxa;
-            if (dx + k < L.xmax) {
-                h0[k] = pick_byte(u0, u1, u2, o) * e[k].a0 + pick_byte(u0, u1, u2, o + 1) * e[k].a1;
-                h1[k] = pick_byte(v0, v1, v2, o) * e[k].a0 + pick_byte(v0, v1, v2, o + 1) * e[k].a1;
-            } else {
-                h0[k] = pick_byte(u0, u1, u2, o) * 2048;
-                h1[k] = pick_byte(v0, v1, v2, o) * 2048;
+        for (int k = 0; k < kRsSlots; ++k) {
+            const int i = base + t + 256 * k;
+            v[k] = i < ndw ? gsrc[i] : 0u;
+        }
+        if (base == 0) {
+            const uint4* xg = (const uint4*)(xt + L.xtab_off);  // xtab_off is a multiple of 4
+            for (int gi = t; gi < ngrp; gi += 256) {
+                const uint4 q0 = xg[2 * gi], q1 = xg[2 * gi + 1];
+                const uint32_t sx0 = q0.x;
+                // byte r and r + 1 of the window as a u16 pair (selector 0x0c = zero byte)
+                auto sel = [&](uint32_t sx) { const uint32_t r = sx - sx0; return r | ((r + 1) << 16) | 0x0c000c00u; };
+                s_sel[gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+                s_aa[gi] = uint4{q0.y, q0.w, q1.y, q1.w};
+                s_sx0[gi] = (int)sx0;
             }
+            if (t < 3 * nrow) s_ry[t] = ((const uint32_t*)(yt + L.ytab_off + dy0))[t];
         }
-    } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int sx = e[k > last ? last : k].sx;
-            if (dx + k < L.xmax) {
-                h0[k] = r0[sx] * e[k].a0 + r0[sx + 1] * e[k].a1;
-                h1[k] = r1[sx] * e[k].a0 + r1[sx + 1] * e[k].a1;
-            } else {
-                h0[k] = r0[sx] * 2048;
-                h1[k] = r1[sx] * 2048;
-            }
+        for (int k = 0; k < kRsSlots; ++k) {
+            const int i = base + t + 256 * k;
+            if (i < ndw) s_src[i] = v[k];
         }
     }
-    uint32_t word = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        int v;
-        if (dx + k < L.xvec) {  // OpenCV VResizeLinearVec_32s8u: v_mul_hi on (S>>4) packed to int16, (x+2)>>2
-            const int a0 = min(h0[k] >> 4, 32767), a1 = min(h1[k] >> 4, 32767);
-            v = (((a0 * ry.b0) >> 16) + ((a1 * ry.b1) >> 16) + 2) >> 2;
-        } else {                // FixedPtCast<int, uchar, 22>
-            v = (h0[k] * ry.b0 + h1[k] * ry.b1 + (1 << 21)) >> 22;
-        }
-        word |= (uint32_t)min(max(v, 0), 255) << (8 * k);
+    if (V == 2 && t < 3 * nrow) s_ry[t] = ((const uint32_t*)(yt + L.ytab_off + dy0))[t];
+    __syncthreads();
+    uint8_t* dst = ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy0 * L.pitch;
+    if (V == 1) {
+        if (t == 0) dst[0] = ((const uint8_t*)s_src)[sh0];
+        return;
     }
-    *(uint32_t*)(ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy * L.pitch + dx) = word;
+    const uint8_t* lsrc = (const uint8_t*)s_src;
+    const int step_r = 256 / ngrp, step_g = 256 - step_r * ngrp;
+    int rr = t / ngrp, grp = t - rr * ngrp;
+    while (rr < nrow) {
+        const ResizeY ry = ((const ResizeY*)s_ry)[rr];
+        const uint4 e = s_sel[grp], aa = s_aa[grp];
+        const int sx0 = s_sx0[grp];
+        auto taps = [&](int sy, uint32_t (&h)[4]) {
+            const int A = sh0 + (sy - ys_lo) * sstride + sx0, o = A & 3;
+            const uint32_t* w = (const uint32_t*)(lsrc + (A - o));
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+            // S[sx] * a0 + S[sx + 1] * a1 (a1 = 0 past xmax: OpenCV's S[sx] * 2048)
+            h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
+                                          __builtin_bit_cast(us2, aa.x), 0u, false);
+            h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
+                                          __builtin_bit_cast(us2, aa.y), 0u, false);
+            h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
+                                          __builtin_bit_cast(us2, aa.z), 0u, false);
+            h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                          __builtin_bit_cast(us2, aa.w), 0u, false);
+        };
+        uint32_t h0[4], h1[4];
+        taps(ry.sy0, h0);
+        taps(ry.sy1, h1);
+        // OpenCV VResizeLinearVec_32s8u: v_mul_hi(S >> 4, beta) on int16 lanes, (x + 2) >> 2; h >> 4 <= 32640 so
+        // the int16 pack never saturates and (x * b) >> 16 == mul_hi(x, b << 16); the result is <= 255
+        const uint32_t B0 = (uint32_t)ry.b0 << 16, B1 = (uint32_t)ry.b1 << 16;
+        const int dx = 4 * grp;
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] >> 4, B0) + __umulhi(h1[k] >> 4, B1) + 2) >> 2;
+        if (dx + 3 >= L.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (dx + k >= L.xvec) v[k] = (h0[k] * (uint32_t)ry.b0 + h1[k] * (uint32_t)ry.b1 + (1u << 21)) >> 22;
+        }
+        // pixels past L.w land in the row's pitch padding
+        *(uint32_t*)(dst + rr * L.pitch + dx) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        rr += step_r;
+        grp += step_g;
+        if (grp >= ngrp) {
+            grp -= ngrp;
+            ++rr;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------- k_detect
@@ -1256,9 +1287,11 @@ __global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restric
 
 // ------------------------------------------------------------------------------- launchers
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
-                         const ResizeY* yt, int n_images, hipStream_t s) {
-    dim3 grid((g.lv[l].w + 1023) / 1024, g.lv[l].h, n_images);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, g, l, in, in_pitch, ws, xt, yt);
+                         const ResizeY* yt, int n_images, hipStream_t s, int variant) {
+    dim3 grid((g.lv[l].h + kRsRows - 1) / kRsRows, n_images);
+    const size_t lds = (size_t)g.rs_ngrp * 36 + 16 * kRsRows + (size_t)g.rs_nsrc * g.rs_sp + 16;
+    auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;
+    hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();
 }
 
