@@ -82,8 +82,10 @@ struct Geo {
     int rs_sp;           // k_resize: largest source row stride (W for the input, pitch for derived levels)
     int rs_ngrp;         // k_resize: most 4-pixel groups in a derived level row (multiple of 4)
     int max_rh;          // largest FAST cell ROI height (rows)
+    int max_rw;          // largest FAST cell ROI width (columns)
     int max_wh;          // largest FAST detection window height (rows)
     int max_win;         // largest FAST detection window (pixels), rounded up to 16
+    int fd_mp;           // k_detect: M map pitch in u16 (>= widest window + 6, multiple of 8)
     int umax[16];
     float scale[kMaxLevels];
     float inv_scale[kMaxLevels];

@@ -316,12 +316,15 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     cg.x1 = (int16_t)(int)maxXc;
                     cg.y1 = (int16_t)(int)maxYc;
                     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
-                    // k_detect stages a ROI row as 16 re-aligned dwords (<= 64 px)
-                    if (rw > 64 || rh > 64) throw Error(ORBFE_EINVAL, "FAST cell ROI larger than 64 px");
+                    // k_detect stages a ROI row from column -1 as 16 re-aligned dwords (<= 63 px)
+                    if (rw > 63 || rh > 64) throw Error(ORBFE_EINVAL, "FAST cell ROI larger than 63 x 64 px");
+                    if (cg.x0 < 1) throw Error(ORBFE_EINVAL, "FAST cell ROI at column 0");
                     const int ww = std::max(rw - 6, 0), wh = std::max(rh - 6, 0);
                     g.max_rh = std::max(g.max_rh, rh);
+                    g.max_rw = std::max(g.max_rw, rw);
                     g.max_wh = std::max(g.max_wh, wh);
                     g.max_win = std::max(g.max_win, (ww * wh + 15) & ~15);
+                    g.fd_mp = std::max(g.fd_mp, (ww + 6 + 7) & ~7);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
                     slot_off += cg.slot_cap;

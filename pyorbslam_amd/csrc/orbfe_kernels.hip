@@ -213,70 +213,99 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 }
 
 // ------------------------------------------------------------------------------- k_detect
-// FAST-9/16 "M" of a pixel: it is a segment-test corner at threshold t iff M > t, and OpenCV's
-// cornerScore is then M - 1.  M = max(v - min_arc max9(I), max_arc min9(I) - v) over the 16 arcs.
-__device__ __forceinline__ int fast_m(const uint8_t* r, int s) {
-    int p[16];
-    p[0] = r[3 * s];
-    p[1] = r[3 * s + 1];
-    p[2] = r[2 * s + 2];
-    p[3] = r[s + 3];
-    p[4] = r[3];
-    p[5] = r[-s + 3];
-    p[6] = r[-2 * s + 2];
-    p[7] = r[-3 * s + 1];
-    p[8] = r[-3 * s];
-    p[9] = r[-3 * s - 1];
-    p[10] = r[-2 * s - 2];
-    p[11] = r[-s - 3];
-    p[12] = r[-3];
-    p[13] = r[s - 3];
-    p[14] = r[2 * s - 2];
-    p[15] = r[3 * s - 1];
-    const int v = r[0];
-    int mx3[16], mn3[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mx3[k] = max(max(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
-        mn3[k] = min(min(p[k], p[(k + 1) & 15]), p[(k + 2) & 15]);
-    }
-    int lo = 255, hi = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        lo = min(lo, max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]));
-        hi = max(hi, min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]));
-    }
-    return max(max(v - lo, hi - v), 0);
+// One wavefront per (cell, image).  FAST "M" of a pixel:
+//   M = max(v - min_arc max9, max_arc min9 - v) over the 16 arcs of 9 contiguous circle pixels;
+//   the pixel is a segment-test corner at threshold t iff M > t, and OpenCV's cornerScore is M - 1.
+// Work is done on horizontal pixel pairs (x, x + 1), x even, in packed f16: pixel values live in LDS as
+// u16 0x3C00 | p, normal f16 numbers in [1, 2) ordered exactly like p, so v_pk_maximum3/minimum3_f16
+// are exact and differences of the raw u16 bits are differences of p.
+//  1. ROI -> LDS (u16, pitch RP, ROI column c at index c + 1 so even window columns are dword
+//     aligned): 16 lanes per row read 16 dwords from the 4-byte aligned start of column -1, re-aligned
+//     with v_alignbyte and widened with v_perm; all loads issued before the first wait.
+//  2. Pre-test, every pair: P = max(v - min_k max(c_k, c_k+1), max_k min(c_k, c_k+1) - v) over the
+//     circularly adjacent cardinal pairs (circle points 0, 4, 8, 12) bounds M from above, because every
+//     arc of 9 contains such a pair.  Pairs with P <= tq = min(iniTh, minTh) in both pixels have M <= tq:
+//     neither corners nor relevant NMS neighbours at either threshold; they keep M = 0.  The others are
+//     queued in row-major order (ballot + mbcnt).
+//  3. Exact M of the queued pairs -> a biased u16 M map with a zero (0x3C00) border; pixels with
+//     M > max(tq, 1) are queued (row-major: two ballots per step) for NMS.
+//  4. NMS over that queue.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the
+//     window or not corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour
+//     with M <= t is below M anyway.  So the local-max test is threshold independent and the
+//     iniTh -> minTh fallback (ORBextractor.cpp:811-815) only changes the cut M > max(t, 1).  Kept
+//     pixels are written in the queue's row-major order, i.e. cv::FAST's output order.
+typedef _Float16 fd_h2 __attribute__((ext_vector_type(2)));
+typedef short fd_s2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ fd_h2 fd_h(uint32_t v) { return __builtin_bit_cast(fd_h2, v); }
+__device__ __forceinline__ fd_s2 fd_s(fd_h2 v) { return __builtin_bit_cast(fd_s2, v); }
+__device__ __forceinline__ fd_h2 fd_max(fd_h2 a, fd_h2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ fd_h2 fd_min(fd_h2 a, fd_h2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ fd_h2 fd_max3(fd_h2 a, fd_h2 b, fd_h2 c) { return fd_max(fd_max(a, b), c); }
+__device__ __forceinline__ fd_h2 fd_min3(fd_h2 a, fd_h2 b, fd_h2 c) { return fd_min(fd_min(a, b), c); }
+template <int DX>
+__device__ __forceinline__ fd_h2 fd_pair(const uint32_t* q) {  // u16 pair at column offset DX
+    if constexpr ((DX & 1) == 0) return fd_h(q[DX / 2]);
+    else return fd_h(__builtin_amdgcn_alignbyte(q[(DX + 1) / 2], q[(DX - 1) / 2], 2));
 }
 
-// FAST "M" on a pitch-64 LDS image: every circle offset is an immediate.
-__device__ __forceinline__ int fast_m64(const uint8_t* r) {
-    return fast_m(r, 64);
+// Upper bound P of M for the pixel pair at dword R (row stride S dwords), as int16 x2.
+template <int S>
+__device__ __forceinline__ fd_s2 fast_bound_pair(const uint32_t* R) {
+    const fd_h2 c0 = fd_pair<0>(R + 3 * S), c1 = fd_pair<3>(R), c2 = fd_pair<0>(R - 3 * S), c3 = fd_pair<-3>(R);
+    const fd_h2 a = fd_min(fd_min3(fd_max(c0, c1), fd_max(c1, c2), fd_max(c2, c3)), fd_max(c3, c0));
+    const fd_h2 b = fd_max(fd_max3(fd_min(c0, c1), fd_min(c1, c2), fd_min(c2, c3)), fd_min(c3, c0));
+    const fd_s2 v = __builtin_bit_cast(fd_s2, R[0]);
+    return __builtin_elementwise_max(v - fd_s(a), fd_s(b) - v);
 }
 
-// One wavefront per (cell, image).
-//  1. ROI -> LDS at a fixed pitch of 64 (ROI pixel (r, c) at r*64 + c): each row is read as 17 dwords
-//     from its 4-byte aligned start and re-aligned with v_alignbyte; all loads are issued before the
-//     first wait.
-//  2. Pre-test at t = min(iniTh, minTh): an arc of 9 contiguous circle pixels always contains two
-//     circularly adjacent cardinals (0,4,8,12), so both must be darker than v - t (or both brighter
-//     than v + t).  Failing pixels have M <= t: neither corners nor relevant NMS neighbours at either
-//     threshold; they keep M = 0.  Survivors are compacted (ballot + mbcnt) into an LDS queue.
-//  3. Exact M of the queued pixels, all lanes busy, written into a zero-bordered pitch-64 M map.
-//  4. NMS.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the window or not
-//     corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour with M <= t
-//     is below M anyway.  So the local-max test is threshold independent and the iniTh -> minTh
-//     fallback (ORBextractor.cpp:811-815) only changes the final cut M > max(t, 1).  Kept pixels are
-//     written in row-major order (ballot-ordered), i.e. cv::FAST's output order.
-// Window pixels map to lanes 32 per row when the window is at most 32 wide (2 rows per step), else 64.
-template <int V>
+// Exact M of the pixel pair at dword R (row stride S dwords), as biased u16 x2.
+template <int S>
+__device__ __forceinline__ uint32_t fast_m_pair(const uint32_t* R) {
+    const fd_h2 p[16] = {fd_pair<0>(R + 3 * S),  fd_pair<1>(R + 3 * S),  fd_pair<2>(R + 2 * S),  fd_pair<3>(R + S),
+                         fd_pair<3>(R),          fd_pair<3>(R - S),      fd_pair<2>(R - 2 * S),  fd_pair<1>(R - 3 * S),
+                         fd_pair<0>(R - 3 * S),  fd_pair<-1>(R - 3 * S), fd_pair<-2>(R - 2 * S), fd_pair<-3>(R - S),
+                         fd_pair<-3>(R),         fd_pair<-3>(R + S),     fd_pair<-2>(R + 2 * S), fd_pair<-1>(R + 3 * S)};
+    fd_h2 mx3[16], mn3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mx3[k] = fd_max3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+        mn3[k] = fd_min3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+    }
+    fd_h2 lo = fd_max3(mx3[0], mx3[3], mx3[6]), hi = fd_min3(mn3[0], mn3[3], mn3[6]);
+#pragma unroll
+    for (int k = 1; k < 15; k += 2) {
+        lo = fd_min3(lo, fd_max3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]),
+                     fd_max3(mx3[k + 1], mx3[(k + 4) & 15], mx3[(k + 7) & 15]));
+        hi = fd_max3(hi, fd_min3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]),
+                     fd_min3(mn3[k + 1], mn3[(k + 4) & 15], mn3[(k + 7) & 15]));
+    }
+    lo = fd_min(lo, fd_max3(mx3[15], mx3[2], mx3[5]));
+    hi = fd_max(hi, fd_min3(mn3[15], mn3[2], mn3[5]));
+    const fd_s2 v = __builtin_bit_cast(fd_s2, R[0]);
+    const fd_s2 m = __builtin_elementwise_max(__builtin_elementwise_max(v - fd_s(lo), fd_s(hi) - v), fd_s2{0, 0});
+    return __builtin_bit_cast(uint32_t, m) | 0x3C003C00u;
+}
+
+__device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
+
+__device__ __forceinline__ int lanes_below(uint64_t b) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+}
+
+// V: 0 full kernel; ablations for tools/microbench.py: 1 ROI staging only, 2 + pre-test, 3 + M.
+// RP: ROI pitch in u16 (48, 64 or 96; >= widest ROI + 3).
+template <int V, int RP>
 __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
+    constexpr int S = RP / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint8_t* roi = lds;                                   // max_rh rows x 64
-    uint8_t* mm = roi + 64 * g.max_rh;                    // (max_wh + 2) rows x 64, zero border
-    uint16_t* queue = (uint16_t*)(mm + 64 * (g.max_wh + 2));  // max_win entries (y << 6 | x)
+    uint16_t* roi = (uint16_t*)lds;                            // max_rh rows x RP
+    const int MP = g.fd_mp;
+    uint16_t* mm = roi + RP * g.max_rh;                        // (max_wh + 2) x MP: window px (x, y) at (y + 1) * MP + x + 2
+    uint16_t* pq = mm + MP * (g.max_wh + 2);                   // pair queue: (y << 6) | x
+    uint16_t* nq = pq + g.max_win;                             // NMS queue: (y << 6) | x
     const int c = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
     const CellGeo cg = cells[c];
     int stride;
@@ -286,7 +315,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     // ---- 1. stage the ROI (16 lanes per row, 4 rows per step; up to 16 steps = 64 rows)
     {
         const int d = lane & 15, r0 = lane >> 4;
-        const int ndw = (rw + 3) >> 2;
+        const int ndw = (rw + 4) >> 2;  // columns -1 .. rw-1
         uint32_t lo[16], hi[16];
         int sh[16];
 #pragma unroll
@@ -295,7 +324,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
             lo[k] = hi[k] = 0;
             sh[k] = 0;
             if (r < rh && d < ndw) {
-                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cg.y0 + r) * stride + cg.x0);
+                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cg.y0 + r) * stride + cg.x0 - 1);
                 const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
                 sh[k] = (int)(a & 3);
                 lo[k] = p[d];
@@ -305,12 +334,17 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int r = r0 + 4 * k;
-            if (r < rh && d < ndw)
-                *(uint32_t*)(roi + r * 64 + 4 * d) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            if (r < rh && d < ndw) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+                uint2 u;
+                u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04010400u);
+                u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04030402u);
+                *(uint2*)(roi + r * RP + 4 * d) = u;
+            }
         }
-        // zero the M map (window + 1-pixel border)
+        // the M map with its zero border
         uint32_t* m32 = (uint32_t*)mm;
-        for (int i = lane; i < 16 * (wh + 2); i += 64) m32[i] = 0u;
+        for (int i = lane; i < (MP / 2) * (wh + 2); i += 64) m32[i] = 0x3C003C00u;
     }
     __syncthreads();
     if (V == 1) {  // ablation: ROI staging only
@@ -321,72 +355,84 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = 0;
         return;
     }
-    const int lshift = ww <= 32 ? 5 : 6;           // lanes per window row: 32 or 64
-    const int lx = lane & ((1 << lshift) - 1), ly = lane >> lshift, rows_per = 64 >> lshift;
     const int tq = min(g.ini_th, g.min_th);
-    // ---- 2. pre-test + queue
-    int nq = 0;
-    for (int y0 = 0; y0 < wh; y0 += rows_per) {
-        const int y = y0 + ly;
-        bool cand = false;
-        if (y < wh && lx < ww) {
-            const uint8_t* r = roi + (y + 3) * 64 + lx + 3;
-            const int v = r[0], lo = v - tq, hi = v + tq;
-            const int c0 = r[3 * 64], c1 = r[3], c2 = r[-3 * 64], c3 = r[-3];
-            const bool d0 = c0 < lo, d1 = c1 < lo, d2 = c2 < lo, d3 = c3 < lo;
-            const bool b0 = c0 > hi, b1 = c1 > hi, b2 = c2 > hi, b3 = c3 > hi;
-            cand = (d0 & d1) | (d1 & d2) | (d2 & d3) | (d3 & d0) | (b0 & b1) | (b1 & b2) | (b2 & b3) | (b3 & b0);
+    // ---- 2. pre-test of every pair (row-major: lane -> pair i = i0 + lane)
+    const int prow = (ww + 1) >> 1, npair = prow * wh;
+    const int step_y = 64 / prow, step_x = 64 - step_y * prow;
+    int npq = 0;
+    {
+        int py = lane / prow, px = lane - (lane / prow) * prow;
+        for (int i0 = 0; i0 < npair; i0 += 64) {
+            bool cand = false;
+            if (i0 + lane < npair) {
+                const int x = 2 * px;
+                const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + (py + 3) * RP + x + 4));
+                cand = pb.x > tq || (pb.y > tq && x + 1 < ww);
+            }
+            const uint64_t bal = __ballot(cand);
+            if (cand) pq[npq + lanes_below(bal)] = (uint16_t)((py << 6) | (2 * px));
+            npq += __popcll(bal);
+            py += step_y;
+            px += step_x;
+            if (px >= prow) {
+                px -= prow;
+                ++py;
+            }
         }
-        const uint64_t bal = __ballot(cand);
-        if (cand)
-            queue[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] =
-                (uint16_t)((y << 6) | lx);
-        nq += __popcll(bal);
     }
     __syncthreads();
-    if (V == 2) {  // ablation: + pre-test / queue
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nq & 0;
+    if (V == 2) {  // ablation: + pre-test / pair queue
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = npq & 0;
         return;
     }
-    // ---- 3. exact M of the survivors
-    for (int k = lane; k < nq; k += 64) {
-        const int q = queue[k], y = q >> 6, x = q & 63;
-        mm[(y + 1) * 64 + x + 1] = (uint8_t)fast_m64(roi + (y + 3) * 64 + x + 3);
+    // ---- 3. exact M of the queued pairs -> M map; NMS candidates -> queue
+    const int tlow = max(tq, 1);
+    int nnq = 0;
+    for (int k0 = 0; k0 < npq; k0 += 64) {
+        bool h0 = false, h1 = false;
+        uint32_t e = 0;
+        if (k0 + lane < npq) {
+            e = pq[k0 + lane];
+            const int x = e & 63, y = e >> 6;
+            uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
+            if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
+            *(uint32_t*)(mm + (y + 1) * MP + x + 2) = m;
+            h0 = (int)(m & 0x3FFu) > tlow;
+            h1 = (int)((m >> 16) & 0x3FFu) > tlow;
+        }
+        const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+        const int o = nnq + lanes_below(b0) + lanes_below(b1);
+        if (h0) nq[o] = (uint16_t)e;
+        if (h1) nq[o + (int)h0] = (uint16_t)(e + 1);
+        nnq += __popcll(b0) + __popcll(b1);
     }
     __syncthreads();
     if (V == 3) {  // ablation: + exact M
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = mm[65] & 0;
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
         return;
     }
-    // ---- 4. NMS (local max) + ordered compaction at iniTh, else minTh
+    // ---- 4. NMS (local max) over the queue + ordered compaction at iniTh, else minTh
     uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
     int total = 0;
-    const int tlow = max(min(g.ini_th, g.min_th), 1);
     for (int pass = 0; pass < 2; ++pass) {
-        const int th = max(pass == 0 ? g.ini_th : g.min_th, 1);
+        const int thb = 0x3C00 + max(pass == 0 ? g.ini_th : g.min_th, 1);
         total = 0;
-        for (int y0 = 0; y0 < wh; y0 += rows_per) {
-            const int y = y0 + ly;
+        for (int k0 = 0; k0 < nnq; k0 += 64) {
             bool keep = false;
-            int m = 0;
-            if (y < wh && lx < ww) {
-                const uint8_t* p = mm + (y + 1) * 64 + lx + 1;
-                m = p[0];
-                if (m > th && m > tlow) {
-                    const int n0 = max(max(p[-65], p[-64]), p[-63]);
-                    const int n1 = max(max(p[-1], p[1]), p[63]);
-                    const int n2 = max(p[64], p[65]);
-                    keep = m > max(max(n0, n1), n2);
-                }
+            int e = 0, own = 0;
+            if (k0 + lane < nnq) {
+                e = nq[k0 + lane];
+                const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
+                own = q[0];
+                const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]), imax3(q[MP - 1], q[MP], q[MP + 1]));
+                keep = own > max(imax3(nmax, q[-1], q[1]), thb);
             }
             const uint64_t bal = __ballot(keep);
-            if (keep) {
-                const int o = total + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-                if (o < cg.slot_cap)
-                    out[o] = (uint32_t)(cg.x0 + lx + 3) | ((uint32_t)(cg.y0 + y + 3) << 12) | ((uint32_t)(m - 1) << 24);
-            }
+            const int o = total + lanes_below(bal);
+            // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+            if (keep && o < cg.slot_cap)
+                out[o] = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
+                         ((uint32_t)((own & 0xFF) - 1) << 24);
             total += __popcll(bal);
         }
         if (total > 0 || g.min_th == g.ini_th) break;
@@ -1295,15 +1341,28 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
     return hipGetLastError();
 }
 
+int detect_rp(const Geo& g) { return g.max_rw + 3 <= 48 ? 48 : g.max_rw + 3 <= 64 ? 64 : 96; }
+
+size_t detect_lds_bytes(const Geo& g) {
+    return 2 * ((size_t)detect_rp(g) * g.max_rh + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.max_win);
+}
+
+template <int RP>
+static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
+                             int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
+    const size_t lds = detect_lds_bytes(g);
+    const dim3 grid(g.ncells, n_images), blk(64);
+    auto k = variant == 1 ? k_detect<1, RP> : variant == 2 ? k_detect<2, RP> : variant == 3 ? k_detect<3, RP>
+                                                                                           : k_detect<0, RP>;
+    hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
+}
+
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
-    const size_t lds = (size_t)64 * g.max_rh + 64 * (g.max_wh + 2) + 2 * g.max_win;
-    const dim3 grid(g.ncells, n_images), blk(64);
-    switch (variant) {
-        case 1: hipLaunchKernelGGL(k_detect<1>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
-        case 2: hipLaunchKernelGGL(k_detect<2>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
-        case 3: hipLaunchKernelGGL(k_detect<3>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots); break;
-        default: hipLaunchKernelGGL(k_detect<0>, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
+    switch (detect_rp(g)) {
+        case 48: launch_detect_rp<48>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant); break;
+        case 64: launch_detect_rp<64>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant); break;
+        default: launch_detect_rp<96>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
     }
     return hipGetLastError();
 }
