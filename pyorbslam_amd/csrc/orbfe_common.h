@@ -55,6 +55,9 @@ struct CellGeo {
 };
 
 // Resize column entry.
+// k_blur output tile (the host counts tiles per level with the same numbers)
+constexpr int kBlurTX = 64, kBlurTY = 58;
+
 struct ResizeX {
     int32_t sx;
     int16_t a0, a1;

@@ -285,7 +285,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         Lg.blur_off = bws;
         bws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
         Lg.blur_tile0 = btile;
-        btile += ((Lg.w + 63) / 64) * ((Lg.h + 31) / 32);
+        btile += ((Lg.w + kBlurTX - 1) / kBlurTX) * ((Lg.h + kBlurTY - 1) / kBlurTY);
         Lg.n_feat = c.n_per_level[l];
         Lg.size = (float)(int)(31 * c.sf[l]);
         // cell grid (ORBextractor.cpp:772-806)

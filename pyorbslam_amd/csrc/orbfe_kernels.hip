@@ -850,16 +850,28 @@ constexpr int kDescWaves = 4;
 // ------------------------------------------------------------------------------- k_blur
 // cv::GaussianBlur(level clone, 7x7, sigma 2, BORDER_REFLECT_101) for every level of every image, the
 // bit-exact 8U fixed-point path: out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
-// One 256-thread workgroup per 64 x 32 output tile.  The 70 x 38 input window (column 0 = X0 - 3) is
-// staged in LDS at pitch 80: interior tiles with 19 re-aligned dwords per row (all loads issued before
-// the first wait), border tiles byte by byte through reflect-101.  Each thread then produces 4 adjacent
-// pixels per pass (horizontal into u16 LDS, vertical into one dword store).
-constexpr int kBlurTX = 64, kBlurTY = 32, kBlurSP = 80;
+// One 256-thread workgroup per kBlurTX x kBlurTY output tile.
+//  * staging: the 64-row x 72-column input window (rows Y0-3 .., columns X0-4 ..) as 18 re-aligned dwords
+//    per row, all loads issued before the first wait; rows go through reflect-101, and the <= 3 columns
+//    left of 0 / right of w-1 of edge tiles are patched in LDS from their reflect-101 sources.
+//  * horizontal: 4 adjacent pixels of 2 rows per thread step, each tap sum = 2 x v_dot4_u32_u8 over
+//    v_alignbyte windows (weights 18,34,48,56 | 48,34,18,0); stored row-pair interleaved, so a dword
+//    holds (H[2m][x], H[2m+1][x]).
+//  * vertical: output rows 2n+3 and 2n+4 of the window from the 4 interleaved dwords P(n) .. P(n+3),
+//    4 x v_dot2_u32_u16 each with the +2^15 rounding as the accumulator seed; 2 aligned dword stores.
+constexpr int kBlurWR = kBlurTY + 6;        // staged window rows (64)
+constexpr int kBlurWD = (kBlurTX + 8) / 4;  // staged dwords per row (18)
+constexpr int kBlurSD = 20;                 // LDS pitch of a staged row, dwords
+
+__device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clamped for far-out rows
+    p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
+    return min(max(p, 0), n - 1);
+}
 
 __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                               const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur) {
-    __shared__ __attribute__((aligned(16))) uint8_t src[(kBlurTY + 6) * kBlurSP];
-    __shared__ __attribute__((aligned(16))) uint16_t hor[(kBlurTY + 6) * kBlurTX];
+    __shared__ __attribute__((aligned(16))) uint32_t src[kBlurWR * kBlurSD];
+    __shared__ __attribute__((aligned(16))) uint32_t hor[(kBlurWR / 2) * kBlurTX];
     const int img = blockIdx.y, t = threadIdx.x;
     int l = 0;
     while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].blur_tile0) ++l;
@@ -870,97 +882,105 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    // interior: no reflection, and the 19th dword (+1 for re-alignment) stays inside the row band
-    const bool interior = X0 >= 3 && X0 + kBlurTX + 3 + 8 <= L.w && Y0 >= 3 && Y0 + kBlurTY + 3 <= L.h;
-    if (interior) {
-        uint32_t lo[3], hi[3];
-        int sh[3], dst[3];
+    {
+        constexpr int NS = (kBlurWR * kBlurWD + 255) / 256;
+        uint32_t lo[NS], hi[NS];
+        int sh[NS], dst[NS];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {  // 38 rows x 19 dwords = 722 slots, 3 per thread
+        for (int k = 0; k < NS; ++k) {
             const int slot = t + 256 * k;
+            const int r = slot / kBlurWD, d = slot - r * kBlurWD;
+            const int x = X0 - 4 + 4 * d;  // image column of the dword's first byte
             dst[k] = -1;
             lo[k] = hi[k] = 0;
             sh[k] = 0;
-            if (slot < (kBlurTY + 6) * 19) {
-                const int r = slot / 19, d = slot - r * 19;
-                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(Y0 - 3 + r) * stride + X0 - 3);
+            if (r < kBlurWR && x >= 0 && x < L.w) {
+                const uint8_t* row = lvl + (int64_t)reflect101c(Y0 - 3 + r, L.h) * stride;
+                const uintptr_t a = (uintptr_t)(row + x);
                 const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
                 sh[k] = (int)(a & 3);
-                lo[k] = p[d];
-                hi[k] = p[d + 1];
-                dst[k] = r * kBlurSP + 4 * d;
+                lo[k] = p[0];
+                if (sh[k] != 0 && (const uint8_t*)(p + 1) < row + L.w) hi[k] = p[1];
+                dst[k] = r * kBlurSD + d;
             }
         }
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            if (dst[k] >= 0) *(uint32_t*)(src + dst[k]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
-    } else {
-        constexpr int SW = kBlurTX + 6;
-        uint8_t v[11];
+        for (int k = 0; k < NS; ++k)
+            if (dst[k] >= 0) src[dst[k]] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+    }
+    const bool left = X0 == 0, right = X0 + kBlurTX + 4 > L.w;
+    if (left || right) {  // patch the reflected columns (sources lie inside the window, never patched)
+        __syncthreads();
+        uint8_t* sb = (uint8_t*)src;
+        uint8_t v[2] = {0, 0};
+        int o[2] = {-1, -1};
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
+        for (int k = 0; k < 2; ++k) {
             const int i = t + 256 * k;
-            v[k] = 0;
-            if (i < (kBlurTY + 6) * SW) {
-                const int r = i / SW, c = i - r * SW;
-                v[k] = lvl[(int64_t)reflect101(Y0 + r - 3, L.h) * stride + reflect101(X0 + c - 3, L.w)];
+            const int r = i / 6, j = i - r * 6;
+            const int x = j < 3 ? j - 3 : L.w + j - 3;  // -3 .. -1, w .. w+2
+            const int c = x - X0 + 4;
+            if (r < kBlurWR && c >= 0 && c < 4 * kBlurWD && ((j < 3 && left) || (j >= 3 && right))) {
+                v[k] = sb[r * 4 * kBlurSD + reflect101(x, L.w) - X0 + 4];
+                o[k] = r * 4 * kBlurSD + c;
             }
         }
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int i = t + 256 * k;
-            if (i < (kBlurTY + 6) * SW) {
-                const int r = i / SW, c = i - r * SW;
-                src[r * kBlurSP + c] = v[k];
-            }
-        }
+        for (int k = 0; k < 2; ++k)
+            if (o[k] >= 0) sb[o[k]] = v[k];
     }
     __syncthreads();
-    // horizontal: 38 rows x 16 groups of 4 columns -> u16
-    for (int i = t; i < (kBlurTY + 6) * 16; i += 256) {
-        const int r = i >> 4, c4 = (i & 15) * 4;
-        const uint32_t* p = (const uint32_t*)(src + r * kBlurSP + c4);
-        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
-        int px[10];
+    constexpr uint32_t K1 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K2 = 48u | (34u << 8) | (18u << 16);
+    // horizontal: (row pair m, group of 4 columns gx): 32 x 16 items, 2 per thread
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            px[b] = (w0 >> (8 * b)) & 0xFF;
-            px[4 + b] = (w1 >> (8 * b)) & 0xFF;
-        }
-        px[8] = w2 & 0xFF;
-        px[9] = (w2 >> 8) & 0xFF;
-        uint32_t o[2];
+    for (int j = 0; j < (kBlurWR / 2) * (kBlurTX / 4) / 256; ++j) {
+        const int it = t + 256 * j, m = it >> 4, gx = it & 15;
+        uint32_t h[2][4];
 #pragma unroll
-        for (int b = 0; b < 4; b += 2) {
-            const uint32_t h0 = 18 * (px[b] + px[b + 6]) + 34 * (px[b + 1] + px[b + 5]) + 48 * (px[b + 2] + px[b + 4]) +
-                                56 * px[b + 3];
-            const uint32_t h1 = 18 * (px[b + 1] + px[b + 7]) + 34 * (px[b + 2] + px[b + 6]) +
-                                48 * (px[b + 3] + px[b + 5]) + 56 * px[b + 4];
-            o[b >> 1] = h0 | (h1 << 16);
+        for (int rr = 0; rr < 2; ++rr) {
+            const uint32_t* q = src + (2 * m + rr) * kBlurSD + gx;
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+            h[rr][0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), K1,
+                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), K2, 0u, false), false);
+            h[rr][1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), K1,
+                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), K2, 0u, false), false);
+            h[rr][2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), K1,
+                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), K2, 0u, false), false);
+            h[rr][3] = __builtin_amdgcn_udot4(d1, K1, __builtin_amdgcn_udot4(d2, K2, 0u, false), false);
         }
-        *(uint2*)(hor + r * kBlurTX + c4) = make_uint2(o[0], o[1]);
+        *(uint4*)(hor + m * kBlurTX + 4 * gx) = uint4{h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
+                                                       h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
     }
     __syncthreads();
+    // vertical: (output row pair n, group gx): window rows 2n+3, 2n+4 = tile rows 2n, 2n+1
     uint8_t* dstimg = blur + (int64_t)img * g.blur_bytes + L.blur_off;
-    for (int i = t; i < kBlurTY * 16; i += 256) {
-        const int r = i >> 4, c4 = (i & 15) * 4;
-        const int y = Y0 + r, x = X0 + c4;
+    auto w2 = [](uint32_t a, uint32_t b) { return __builtin_bit_cast(us2, a | (b << 16)); };
+    for (int it = t; it < (kBlurTY / 2) * (kBlurTX / 4); it += 256) {
+        const int n = it >> 4, gx = it & 15;
+        const int y = Y0 + 2 * n, x = X0 + 4 * gx;
         if (y >= L.h || x >= L.w) continue;
-        uint32_t acc[4] = {0, 0, 0, 0};
+        uint4 P[4];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            const uint2 q = *(const uint2*)(hor + (r + j) * kBlurTX + c4);
-            const uint32_t kj = j == 3 ? 56 : (j == 2 || j == 4) ? 48 : (j == 1 || j == 5) ? 34 : 18;
-            acc[0] += kj * (q.x & 0xFFFF);
-            acc[1] += kj * (q.x >> 16);
-            acc[2] += kj * (q.y & 0xFFFF);
-            acc[3] += kj * (q.y >> 16);
+        for (int k = 0; k < 4; ++k) P[k] = *(const uint4*)(hor + (n + k) * kBlurTX + 4 * gx);
+        uint32_t e = 0, o = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t p0 = (&P[0].x)[c], p1 = (&P[1].x)[c], p2 = (&P[2].x)[c], p3 = (&P[3].x)[c];
+            uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(18, 34), 32768u, false);
+            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(48, 56), a, false);
+            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(48, 34), a, false);
+            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(18, 0), a, false);
+            uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(0, 18), 32768u, false);
+            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(34, 48), b, false);
+            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(56, 48), b, false);
+            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(34, 18), b, false);
+            e |= (a >> 16) << (8 * c);
+            o |= (b >> 16) << (8 * c);
         }
-        uint32_t word = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) word |= ((acc[b] + 32768u) >> 16) << (8 * b);
-        // rows are padded to a 16-byte pitch, so the dword never leaves the row's allocation
-        *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = word;
+        // rows are padded to a 16-byte pitch, so the dwords never leave the row's allocation
+        *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = e;
+        if (y + 1 < L.h) *(uint32_t*)(dstimg + (int64_t)(y + 1) * L.pitch + x) = o;
     }
 }
 
