@@ -41,7 +41,6 @@ struct LevelGeo {
     int xtab_off, ytab_off;
     int xmax;            // first column whose sx+1 >= src width
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
-    int chunk0;          // first k_describe block of this level (4 keypoints per block)
     int64_t blur_off;    // byte offset of the blurred level inside an image's blur workspace
     int blur_tile0;      // first k_blur tile of this level (64 x 32 tiles)
 };

@@ -96,13 +96,11 @@ struct orbfe_ctx {
     std::vector<CellGeo> cells;
     std::vector<ResizeX> xt;
     std::vector<ResizeY> yt;
-    std::vector<int> chunk_level;
     int maxcell = 0;
 
     DevBuf<CellGeo> d_cells;
     DevBuf<ResizeX> d_xt;
     DevBuf<ResizeY> d_yt;
-    DevBuf<int> d_chunk_level;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
     DevBuf<uint8_t> d_blur;
@@ -259,10 +257,9 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.cells.clear();
     c.xt.clear();
     c.yt.clear();
-    c.chunk_level.clear();
     c.maxcell = 0;
     int64_t ws = 0, bws = 0;
-    int kp_off = 0, key_off = 0, chunk = 0, btile = 0;
+    int kp_off = 0, key_off = 0, btile = 0;
     int64_t slot_off = 0;
     for (int l = 0; l < L; ++l) {
         LevelGeo& Lg = g.lv[l];
@@ -351,10 +348,6 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         Lg.kp_cap = std::max(Lg.n_feat + 2, 4 * Lg.n_ini) + 2;
         Lg.kp_off = kp_off;
         kp_off += Lg.kp_cap;
-        Lg.chunk0 = chunk;
-        const int nch = (Lg.kp_cap + 3) / 4;
-        for (int k = 0; k < nch; ++k) c.chunk_level.push_back(l);
-        chunk += nch;
         g.max_ncap = std::max(g.max_ncap, Lg.kp_cap);
     }
     g.ncells = (int)c.cells.size();
@@ -400,9 +393,6 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.d_yt.ensure(c.yt.size());
         if (!c.yt.empty())
             HIPCK(hipMemcpy(c.d_yt.p, c.yt.data(), c.yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
-        c.d_chunk_level.ensure(c.chunk_level.size());
-        HIPCK(hipMemcpy(c.d_chunk_level.p, c.chunk_level.data(), c.chunk_level.size() * sizeof(int),
-                        hipMemcpyHostToDevice));
         c.have_single = false;
     }
     if (max_images > c.max_images) {
@@ -458,7 +448,7 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     prof_mark(c, s, 3);
     HIPCK(launch_blur(g, d_in, pitch, c.d_ws.p, c.d_blur.p, n, s));
     HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_blur.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p,
-                          c.d_count.p, c.d_chunk_level.p, (int)c.chunk_level.size(), n, s));
+                          c.d_count.p, n, s));
     prof_mark(c, s, 4);
     c.last_in = d_in;
     c.last_pitch = pitch;
@@ -891,8 +881,7 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                         HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s));
                     if (variant != 1)
                         HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
-                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p,
-                                              h->d_chunk_level.p, (int)h->chunk_level.size(), n, s));
+                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, n, s));
                     break;
                 case 4:
                     if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");

@@ -19,15 +19,30 @@
 
 namespace orbfe {
 
-__constant__ int8_t c_pattern[1024] = {
+// (x0, y0, x1, y1) of the 256 point pairs as floats: lane j reads bits j + 64 i as 4 x 16-byte loads
+__constant__ __attribute__((aligned(16))) float c_pattern[1024] = {
 #include "brief_pattern.inc"
 };
 
 // ------------------------------------------------------------------------------- small helpers
+// Buffer resource for a wave-uniform base pointer: loads take a 32-bit lane offset (no 64-bit address
+// arithmetic per lane).  Dword 3 = 0x00020000, the gfx9 raw-buffer format word.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
+}
+
+// Wave-wide sum (wave-uniform result): DPP quad_perm / row_ror sums inside each 16-lane row, then the
+// four row sums through v_readlane (no LDS-crossbar round trips).
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
 }
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -985,107 +1000,160 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------- k_describe
-// One wavefront per keypoint, registers only.
-//  IC_Angle (:77-104): the 31 x 31 square around the keypoint is read as 31 rows x 9 aligned dwords
-//  (5 loads per lane, all issued before the first use); each lane accumulates m10 = sum u*I and
-//  m01 = sum v*I over its bytes that fall inside the umax disc; two wave reductions.
-//  computeOrbDescriptor (:108-147): lane j evaluates bits j, j+64, j+128, j+192, i.e. 8 rotated
-//  samples gathered straight from the blurred level (k_blur), assembled by __ballot.
+// IC_Angle (ORBextractor.cpp:77-104) + steered BRIEF on the blurred level (:108-147) for every kept
+// keypoint, in the output order of the reference (levels ascending, octree order inside a level).
+// Four keypoints per wavefront, 16 lanes each (row q = lane >> 4 of the wave, sub-lane s = lane & 15);
+// a wave's 4 keypoints are consecutive in one level, so level data stays wave-uniform and the
+// wave-uniform scalar work (fastAtan2, the glibc sincosf replica in f64) is paid once per 4 keypoints.
+//  centroid: the 31 x 31 square as 31 rows x 9 aligned dwords, 18 per lane, all issued before the
+//  first use; per dword, the bytes inside the umax disc as a byte mask, then sum(val) and sum(b * val)
+//  by v_dot4_u32_u8: m10 += u0 * S0 + S1, m01 += v * S0; DPP sums over the 16-lane row.
+//  descriptor: sub-lane s evaluates bits s + 16 i (i = 0..15): 32 rotated samples (the reference's FMA
+//  contraction, cvRound = half-even) from the blurred level; round i's ballot is the 16-bit chunk i of
+//  each row's descriptor, kept by sub-lane i and stored as one u16 per lane.
+// Blocks are remapped XCD-aware: each XCD's L2 receives a contiguous run of waves (consecutive
+// keypoints are spatial neighbours in octree order and share cache lines).
+__device__ __forceinline__ int row16_sum(int v) {  // sum over the lane's 16-lane DPP row
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                   const uint8_t* __restrict__ ws, const uint8_t* __restrict__ blur,
                                                   const uint32_t* __restrict__ lvl_kp,
                                                   const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
-                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
-                                                  const int* __restrict__ chunk_level) {
+                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count) {
     __shared__ int s_umax[16];
-    const int img = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ float4 s_pat[256];
+    // XCD-aware remap of the flattened grid: hardware block i runs on XCD i % 8
+    const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
+    const int per = nb >> 3;
+    const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;
+    const int img = lb / gridDim.x, blk = lb - img * gridDim.x;
+    const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
+    const int wv = blk * kDescWaves + (threadIdx.x >> 6);
     if (threadIdx.x < 16) s_umax[threadIdx.x] = g.umax[threadIdx.x];
-    int l = 0;  // level of this block from the kernel arguments (no table load)
-    while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].chunk0) ++l;
-    const LevelGeo& L = g.lv[l];
-    const int idx = (blockIdx.x - L.chunk0) * kDescWaves + w;
+    s_pat[threadIdx.x] = ((const float4*)c_pattern)[threadIdx.x];
+    // per level: keypoints (pre) and waves of 4 (wpre), wave-uniform
     const int* cnt = lvl_count + img * g.nlevels;
-    // the packed key can be read before knowing whether idx < count (the slot always exists)
-    const uint32_t key = lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx];
-    int o = idx, n_l = 0, total = 0;
-    for (int i = 0; i < g.nlevels; ++i) {
-        const int ci = cnt[i];
-        o += i < l ? ci : 0;
-        n_l = i == l ? ci : n_l;
-        total += ci;
+    int pre[kMaxLevels + 1], wpre[kMaxLevels + 1];
+    pre[0] = wpre[0] = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxLevels; ++i) {
+        const int c = i < g.nlevels ? cnt[i] : 0;
+        pre[i + 1] = pre[i] + c;
+        wpre[i + 1] = wpre[i] + ((c + 3) >> 2);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) out_count[img] = total;
+    if (blk == 0 && threadIdx.x == 0) out_count[img] = pre[kMaxLevels];
     __syncthreads();
-    if (idx >= n_l) return;  // wave-uniform; no barrier follows
+    if (wv >= wpre[kMaxLevels]) return;  // wave-uniform; no barrier follows
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxLevels; ++i) l += (i < g.nlevels && wv >= wpre[i]) ? 1 : 0;
+    const LevelGeo& L = g.lv[l];
+    const int n_l = pre[l + 1] - pre[l];
+    const int idx = 4 * (wv - wpre[l]) + q;  // keypoint of this row inside level l
+    const bool valid = idx < n_l;
+    const int o = pre[l] + idx;
+    const uint32_t key = valid ? lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx] : (20u | (20u << 12));
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
     const int cx = key & 0xFFF, cy = (key >> 12) & 0xFFF, score = key >> 24;
-    // ---- intensity centroid
-    uint32_t word[5];
-    int shv[5];
+    // ---- intensity centroid: 18 dwords per lane, buffer loads at 32-bit offsets from the level base
+    const uint32_t off0 = (uint32_t)((cy - kHalfPatch) * stride + cx - kHalfPatch);
+    const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
+    const __amdgpu_buffer_rsrc_t lr = uniform_rsrc(lvl);
+    const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;  // provably 24-bit: v_mul_u32_u24, full rate
+    constexpr int NW = (31 * 9 + 15) / 16;
+    // slot sl + 16 k of the 31 x 9 window -> (row r, dword d), stepped without division (16 = 9 + 7)
+    int rk[NW], dk[NW];
+    {
+        int r = sl >= 9 ? 1 : 0, d = sl - 9 * r;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const int slot = lane + 64 * k;
-        word[k] = 0;
-        shv[k] = 0;
-        if (slot < 31 * 9) {
-            const int r = slot / 9, d = slot - r * 9;
-            const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cy - kHalfPatch + r) * stride + cx - kHalfPatch);
-            shv[k] = (int)(a & 3);
-            word[k] = ((const uint32_t*)(a & ~(uintptr_t)3))[d];
-        }
-    }
-    int m10 = 0, m01 = 0;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const int slot = lane + 64 * k;
-        if (slot < 31 * 9) {
-            const int r = slot / 9, d = slot - r * 9;
-            const int v = r - kHalfPatch, av = v < 0 ? -v : v;
-            const int um = s_umax[av];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int u = 4 * d + b - shv[k] - kHalfPatch;
-                if (u >= -um && u <= um) {
-                    const int val = (word[k] >> (8 * b)) & 0xFF;
-                    m10 += u * val;
-                    m01 += v * val;
-                }
+        for (int k = 0; k < NW; ++k) {
+            rk[k] = r;
+            dk[k] = d;
+            d += 7;
+            r += 1;
+            if (d >= 9) {
+                d -= 9;
+                r += 1;
             }
         }
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
+    uint32_t word[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        word[k] = 0;
+        if (rk[k] < 31) {
+            const uint32_t off = off0 + (uint32_t)rk[k] * stride24;
+            word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * dk[k] - (lvl_lo & 3u), 0, 0);
+        }
+    }
+    // m10 = sum (u0 + b) val_b, m01 = sum v val_b with non-negative byte weights (u0 + 18 + b), (v + 15)
+    // accumulated by v_dot4 and corrected by -18 / -15 x sum(val)
+    uint32_t a10 = 0, a01 = 0, a1 = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        if (rk[k] < 31) {
+            const int r = rk[k], d = dk[k];
+            const int sh = (int)((lvl_lo + off0 + (uint32_t)r * stride24) & 3u);
+            const int v = r - kHalfPatch, um = s_umax[v < 0 ? -v : v];
+            const int u0 = 4 * d - sh - kHalfPatch;  // u of byte 0
+            const int blo = min(max(-um - u0, 0), 4), bhi = min(max(um - u0 + 1, 0), 4);
+            const int n = bhi - blo;
+            const uint32_t mask = n > 0 ? (0xFFFFFFFFu >> (32 - 8 * n)) << (8 * blo) : 0u;
+            const uint32_t mw = word[k] & mask;
+            // byte broadcasts by v_perm (selector 0 = byte 0 of the second source in every byte)
+            a10 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)(u0 + 18), 0u) + 0x03020100u, a10, false);
+            a01 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)(v + 15), 0u), a01, false);
+            a1 = __builtin_amdgcn_udot4(mw, 0x01010101u, a1, false);
+        }
+    }
+    int m10 = (int)a10 - 18 * (int)a1, m01 = (int)a01 - 15 * (int)a1;
+    m10 = row16_sum(m10);
+    m01 = row16_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
-    // ---- steered BRIEF on the blurred level
-    const float factorPI = (float)(M_PI / 180.f);
     float b, a;
-    glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
-    const uint8_t* bl = blur + (int64_t)img * g.blur_bytes + L.blur_off + (int64_t)cy * L.pitch + cx;
-    int val[8];
+    glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
+    // ---- steered BRIEF: 32 samples per lane (|offset| <= 13 * sqrt 2 < 19), 32-bit offsets from the
+    // corner (cy - 19, cx - 19), which is >= 0: detection windows start 19 pixels inside every level
+    const __amdgpu_buffer_rsrc_t br = uniform_rsrc(blur + (int64_t)img * g.blur_bytes + L.blur_off);
+    const uint32_t boff0 = (uint32_t)((cy - 19) * L.pitch + cx - 19), pitch24 = (uint32_t)L.pitch & 0xFFFFFFu;
+    int val[32];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int bit = (k >> 1) * 64 + lane;
-        const float px = (float)c_pattern[4 * bit + 2 * (k & 1)], py = (float)c_pattern[4 * bit + 2 * (k & 1) + 1];
-        const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
-        const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
-        val[k] = bl[rr * L.pitch + cc];
-    }
-    uint64_t* dst = (uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32);
+    for (int i = 0; i < 16; ++i) {
+        const float4 pt = s_pat[sl + 16 * i];
 #pragma unroll
-    for (int rnd = 0; rnd < 4; ++rnd) {
-        const uint64_t m = __ballot(val[2 * rnd] < val[2 * rnd + 1]);
-        if (lane == 0) dst[rnd] = m;
+        for (int e = 0; e < 2; ++e) {
+            const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
+            const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
+            const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
+            val[2 * i + e] = __builtin_amdgcn_raw_buffer_load_b8(
+                br, boff0 + ((uint32_t)(rr + 19) & 0xFFu) * pitch24 + (uint32_t)(cc + 19), 0, 0);
+        }
     }
-    if (lane == 0) {
-        orbfe_keypoint kp;
-        kp.x = l ? __fmul_rn((float)cx, L.scale) : (float)cx;
-        kp.y = l ? __fmul_rn((float)cy, L.scale) : (float)cy;
-        kp.size = L.size;
-        kp.angle = angle;
-        kp.response = (float)score;
-        kp.octave = l;
-        out_kp[(int64_t)img * g.kp_cap + o] = kp;
+    uint64_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint64_t m = __ballot(val[2 * i] < val[2 * i + 1]);
+        mine = sl == i ? m : mine;
+    }
+    if (valid) {
+        *(uint16_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 2 * sl) = (uint16_t)(mine >> (16 * q));
+        if (sl == 0) {
+            orbfe_keypoint kp;
+            kp.x = l ? __fmul_rn((float)cx, L.scale) : (float)cx;
+            kp.y = l ? __fmul_rn((float)cy, L.scale) : (float)cy;
+            kp.size = L.size;
+            kp.angle = angle;
+            kp.response = (float)score;
+            kp.octave = l;
+            out_kp[(int64_t)img * g.kp_cap + o] = kp;
+        }
     }
 }
 
@@ -1411,9 +1479,11 @@ hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const 
 
 hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
                            const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
-                           int* out_count, const int* chunk_level, int n_chunks, int n_images, hipStream_t s) {
-    hipLaunchKernelGGL(k_describe, dim3(n_chunks, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur, lvl_kp,
-                       lvl_count, out_kp, out_desc, out_count, chunk_level);
+                           int* out_count, int n_images, hipStream_t s) {
+    int waves = 0;  // most waves an image can need: 4 keypoints per wave, per level
+    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + 3) / 4;
+    hipLaunchKernelGGL(k_describe, dim3((waves + kDescWaves - 1) / kDescWaves, n_images), dim3(256), 0, s, g, in,
+                       in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count);
     return hipGetLastError();
 }
 
