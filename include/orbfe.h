@@ -199,6 +199,9 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
  *   (ORBextractor.cpp:833-834), as (x_rel, y_rel, score) triples. */
 int orbfe_debug_candidates(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out);
 int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t cap, int32_t* n_out);
+/* orbfe_debug_octree_profile: re-runs the last batch's octree stage with wall-clock marks (100 MHz ticks,
+ * 64 per (image, level), 0 = not reached) written by each workgroup's first thread; development aid. */
+int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n);
 
 #ifdef __cplusplus
 }

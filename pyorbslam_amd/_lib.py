@@ -62,6 +62,7 @@ SIGNATURES = {
     "orbfe_microbench": [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)],
     "orbfe_debug_candidates": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
+    "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
 }
 
 _lib: C.CDLL | None = None

@@ -874,7 +874,7 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                     break;
                 case 2:
                     HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_kd.p, h->d_kn.p,
-                                        h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s));
+                                        h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
                     if (variant != 2)
@@ -948,6 +948,23 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
             xyr[3 * i + 1] = (int)((kp[i] >> 12) & 0xFFF) - kBorder;
             xyr[3 * i + 2] = (int)(kp[i] >> 24);
         }
+    });
+}
+
+int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n) {
+    return guarded([&] {
+        if (!h || !marks) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->last_images <= 0 || !h->last_in) throw Error(ORBFE_ESTATE, "run a batch first");
+        const Geo& g = h->geo;
+        const int64_t need = (int64_t)h->last_images * g.nlevels * 64;
+        if (n < need) throw Error(ORBFE_ECAPACITY, "buffer too small");
+        DevBuf<long long> d;
+        d.ensure(need);
+        HIPCK(hipMemset(d.p, 0, need * sizeof(long long)));
+        HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_kd.p, h->d_kn.p, h->d_lvl_kp.p,
+                            h->d_lvl_count.p, h->d_overflow.p, h->maxcell, h->last_images, h->last_stream, 0, d.p));
+        HIPCK(hipStreamSynchronize(h->last_stream));
+        HIPCK(hipMemcpy(marks, d.p, need * sizeof(long long), hipMemcpyDeviceToHost));
     });
 }
 

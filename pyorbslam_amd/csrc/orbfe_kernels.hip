@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include "orbfe_common.h"
+#include <type_traits>
+
 #include "orbfe_kernels.h"
 
 namespace orbfe {
@@ -61,15 +63,16 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const u
     return ws + (int64_t)img * g.ws_bytes + g.lv[l].ws_off;
 }
 
-// Block-wide (256 threads) exclusive scan of a[0..n) in LDS, in place; returns the total.
-// Each thread owns a contiguous chunk, so prefixes follow array order.  tmp: 257 ints of LDS.
+// Block-wide exclusive scan of a[0..n) in LDS, in place; returns the total.  The first 256 threads own
+// contiguous chunks, so prefixes follow array order; further threads (blocks of up to 1024) only take
+// part in the barriers.  tmp: 257 ints of LDS.
 __device__ int block_excl_scan(int* a, int n, int* tmp) {
     const int t = threadIdx.x;
     const int per = (n + 255) >> 8;
-    const int b = min(t * per, n), e = min(b + per, n);
+    const int b = t < 256 ? min(t * per, n) : n, e = min(b + per, n);
     int s = 0;
     for (int i = b; i < e; ++i) s += a[i];
-    tmp[t] = s;
+    if (t < 256) tmp[t] = s;
     __syncthreads();
     if (t < 64) {
         const int v0 = tmp[4 * t], v1 = tmp[4 * t + 1], v2 = tmp[4 * t + 2], v3 = tmp[4 * t + 3];
@@ -88,7 +91,7 @@ __device__ int block_excl_scan(int* a, int n, int* tmp) {
         if (t == 63) tmp[256] = inc;
     }
     __syncthreads();
-    int run = tmp[t];
+    int run = t < 256 ? tmp[t] : 0;
     for (int i = b; i < e; ++i) {
         const int v = a[i];
         a[i] = run;
@@ -463,17 +466,37 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
 // phase resolve by node creation order (see oracle/orb_oracle.cpp).
 //
 // LDS layout (dynamic, NC = Geo::max_ncap node slots):
-//   box[2][NC] u64 (x0,y0,x1,y1 int16) | cnt[2][NC] i32 | cnt4[4NC] i32 | cpos[4NC] i32 |
-//   sa[NC] sb[NC] sd[NC] proc[NC] i32 | srt[pow2(NC)] u64 | coff[maxcell+1] i32
+//   box[2][NC] u64 (x0,y0,x1,y1 int16) | cnt[2][NC] i32 | cnt4[4NC] i32 | cpos[4NC] u16 |
+//   sa[NC] sb[NC] sd[NC] proc[NC] i32 | srt[pow2(NC)] u64 | coff[maxcell+1] i32 |
+//   kd[kOctKeys] u32 | kn[kOctKeys] u16   (the candidates, when the level has at most kOctKeys; else they
+//   stay in the global kd/kn arrays)
+constexpr int kOctKeys = 7424;     // with the node arrays: <= 80 KiB, two workgroups per CU
+constexpr int kOctThreads = 512;   // 8 waves: the per-pass candidate loops are latency chains
 struct OctLds {
     uint64_t *box0, *box1;
     int *cnt0, *cnt1;
     int* cnt4;
-    int* cpos;
+    uint16_t* cpos;
     int *sa, *sb, *sd, *proc;
     uint64_t* srt;
     int* coff;
+    uint32_t* kd;
+    uint16_t* kn;
 };
+
+// atomicAdd(&bins[b], 1) for every active lane, aggregated per distinct bin of the wave (ballot +
+// popcount, one LDS atomic per bin): for the first octree passes, where thousands of candidates share
+// a handful of counters and plain LDS atomics serialize.
+__device__ __forceinline__ void wave_bin_add(int* bins, int b, bool active) {
+    uint64_t todo = __ballot(active);
+    while (todo) {
+        const int leader = __builtin_ctzll(todo);
+        const int lb = __shfl(b, leader, 64);
+        const uint64_t same = __ballot(active && b == lb) & todo;
+        if ((threadIdx.x & 63) == leader) atomicAdd(&bins[lb], __popcll(same));
+        todo &= ~same;
+    }
+}
 
 __device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
     const int x = (int)(key & 0xFFFu) - kBorder, y = (int)((key >> 12) & 0xFFFu) - kBorder;
@@ -501,15 +524,28 @@ __device__ __forceinline__ uint64_t child_box(uint64_t box, int q) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict__ cells,
+__global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __restrict__ cells,
                                                 const int* __restrict__ cell_count, const uint32_t* __restrict__ slots,
                                                 uint32_t* __restrict__ kd_all, uint16_t* __restrict__ kn_all,
                                                 uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
-                                                int* __restrict__ overflow, int maxcell) {
+                                                int* __restrict__ overflow, int maxcell, int stop,
+                                                long long* __restrict__ prof) {
+    // stop (tools/microbench.py ablations): 1 after the candidate gather, 2 after the initial columns,
+    // 3 after the full-division phase, 16 + l only level l, 64 + 8 l + n only level l and stop before
+    // pass n; 0 = the whole algorithm
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int scan_tmp[257];
     __shared__ int s_S, s_C, s_phase, s_cur, s_nexp, s_P, s_done;
-    const int l = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+    // grid (image, level): level-major dispatch, the long level-0 workgroups start first
+    const int img = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
+    if (stop >= 16 && stop < 64 && l != stop - 16) return;
+    if (stop >= 64 && l != (stop - 64) / 8) return;
+    // prof (orbfe_debug_octree_profile): 64 wall-clock marks (100 MHz) per (image, level)
+    long long* pm = prof ? prof + ((int64_t)img * g.nlevels + l) * 64 : nullptr;
+    auto mark = [&](int id) {
+        if (pm && t == 0 && id < 64) pm[id] = (long long)wall_clock64();
+    };
+    mark(0);
     const LevelGeo& L = g.lv[l];
     const int NC = g.max_ncap;
     int pow2 = 1;
@@ -523,105 +559,285 @@ __global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict
         d.cnt0 = (int*)p; p += 4 * NC;
         d.cnt1 = (int*)p; p += 4 * NC;
         d.cnt4 = (int*)p; p += 16 * NC;
-        d.cpos = (int*)p; p += 16 * NC;
+        d.cpos = (uint16_t*)p; p += 8 * NC;
         d.sa = (int*)p; p += 4 * NC;
         d.sb = (int*)p; p += 4 * NC;
         d.sd = (int*)p; p += 4 * NC;
         d.proc = (int*)p; p += 4 * NC;
-        d.coff = (int*)p;
+        d.coff = (int*)p; p += 4 * ((maxcell + 4) & ~3);
+        d.kd = (uint32_t*)p; p += 4 * kOctKeys;
+        d.kn = (uint16_t*)p;
     }
     const int N = L.n_feat;
     const int ncell = L.ncell;
-    uint32_t* kd = kd_all + (int64_t)img * g.key_total + L.key_off;
-    uint16_t* kn = kn_all + (int64_t)img * g.key_total + L.key_off;
+    uint32_t* kd_g = kd_all + (int64_t)img * g.key_total + L.key_off;
+    uint16_t* kn_g = kn_all + (int64_t)img * g.key_total + L.key_off;
     uint32_t* out = lvl_kp + (int64_t)img * g.lvl_kp_cap + L.kp_off;
 
     // 1. gather the level's candidates in cell order (= vToDistributeKeys order)
-    for (int i = t; i < ncell; i += 256) d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+    for (int i = t; i < ncell; i += kOctThreads) d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
     __syncthreads();
     const int K = block_excl_scan(d.coff, ncell, scan_tmp);
     if (t == 0) d.coff[ncell] = K;
     __syncthreads();
-    const uint32_t* islots = slots + (int64_t)img * g.slot_total;
-    for (int k = t; k < K; k += 256) {
-        int lo = 0, hi = ncell - 1;  // last cell with coff <= k
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+    // the pass loops below read every candidate several times per pass: keep them in LDS when they fit
+    auto run = [&](auto in_lds) {
+        uint32_t* kd;
+        uint16_t* kn;
+        if constexpr (decltype(in_lds)::value) {
+            kd = d.kd;
+            kn = d.kn;
+        } else {
+            kd = kd_g;
+            kn = kn_g;
         }
-        kd[k] = islots[cells[L.cell0 + lo].slot_off + (k - d.coff[lo])];
-    }
-    // 2. initial columns (:543-584); a key goes to column (size_t)(x / hX)
-    const int nIni = L.n_ini;
-    for (int i = t; i < 4 * NC; i += 256) d.cnt4[i] = 0;
-    __syncthreads();
-    for (int k = t; k < K; k += 256) {
-        const int x = (int)(kd[k] & 0xFFFu) - kBorder;
-        int col = (int)((float)x / L.hx);
-        col = min(col, nIni - 1);
-        atomicAdd(&d.cnt4[col], 1);
-        kn[k] = (uint16_t)col;
-    }
-    __syncthreads();
-    if (t == 0) {
-        int S = 0;
-        for (int i = 0; i < nIni; ++i) {
-            const int n = d.cnt4[i];
-            d.cpos[i] = S;
-            if (n > 0) {
-                d.box0[S] = pack_box((int)(L.hx * (float)i), 0, (int)(L.hx * (float)(i + 1)), L.span_y);
-                d.cnt0[S] = n;
-                ++S;
+        const uint32_t* islots = slots + (int64_t)img * g.slot_total;
+        for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {  // 4 keys per step: their slot loads overlap
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * kOctThreads;
+                v[u] = 0;
+                if (k < K) {
+                    int lo = 0, hi = ncell - 1;  // last cell with coff <= k
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    v[u] = islots[cells[L.cell0 + lo].slot_off + (k - d.coff[lo])];
+                }
             }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u * kOctThreads < K) kd[k0 + u * kOctThreads] = v[u];
         }
-        s_S = S;
-        s_C = 0;
-        s_cur = 0;
-        s_phase = 0;
-        s_done = (S == 0);
-        s_nexp = 0;
-        if (S > NC) { s_done = 1; atomicOr(overflow, 1); }
-    }
-    __syncthreads();
-    for (int k = t; k < K; k += 256) kn[k] = (uint16_t)d.cpos[kn[k]];
-    __syncthreads();
+        mark(1);
+        if (stop == 1) return;
+        // 2. initial columns (:543-584); a key goes to column (size_t)(x / hX)
+        const int nIni = L.n_ini;
+        for (int i = t; i < 4 * NC; i += kOctThreads) d.cnt4[i] = 0;
+        __syncthreads();
+        for (int k0 = 0; k0 < K; k0 += kOctThreads) {  // wave-uniform trip count (ballots inside)
+            const int k = k0 + t;
+            int col = 0;
+            if (k < K) {
+                const int x = (int)(kd[k] & 0xFFFu) - kBorder;
+                col = min((int)((float)x / L.hx), nIni - 1);
+                kn[k] = (uint16_t)col;
+            }
+            wave_bin_add(d.cnt4, col, k < K);
+        }
+        __syncthreads();
+        if (t == 0) {
+            int S = 0;
+            for (int i = 0; i < nIni; ++i) {
+                const int n = d.cnt4[i];
+                d.cpos[i] = S;
+                if (n > 0) {
+                    d.box0[S] = pack_box((int)(L.hx * (float)i), 0, (int)(L.hx * (float)(i + 1)), L.span_y);
+                    d.cnt0[S] = n;
+                    ++S;
+                }
+            }
+            s_S = S;
+            s_C = 0;
+            s_cur = 0;
+            s_phase = 0;
+            s_done = (S == 0);
+            s_nexp = 0;
+            if (S > NC) { s_done = 1; atomicOr(overflow, 1); }
+        }
+        __syncthreads();
+        for (int k = t; k < K; k += kOctThreads) kn[k] = (uint16_t)d.cpos[kn[k]];
+        __syncthreads();
+        mark(2);
+        if (stop == 2) return;
 
-    for (int iter = 0; !s_done; ++iter) {
-        const int S = s_S, C = s_C, cur = s_cur, nxt = cur ^ 1;
-        const uint64_t* box = cur ? d.box1 : d.box0;
-        const int* cnt = cur ? d.cnt1 : d.cnt0;
-        uint64_t* nbox = cur ? d.box0 : d.box1;
-        int* ncnt = cur ? d.cnt0 : d.cnt1;
-        if (iter > 4 * NC + 64) {  // cannot happen (each step grows the list or finishes); never hang
-            if (t == 0) { atomicOr(overflow, 2); s_done = 1; }
-            __syncthreads();
-            break;
-        }
-        if (s_phase == 0) {
-            // ---------------- full pass (:605-664): divide every node holding more than one key
-            for (int i = t; i < 4 * S; i += 256) d.cnt4[i] = 0;
-            if (t == 0) s_nexp = 0;
-            __syncthreads();
-            for (int k = t; k < K; k += 256) {
-                const int p = kn[k];
-                if (cnt[p] > 1) atomicAdd(&d.cnt4[4 * p + quad_of(kd[k], box[p])], 1);
+        for (int iter = 0; !s_done; ++iter) {
+            const int S = s_S, C = s_C, cur = s_cur, nxt = cur ^ 1;
+            const uint64_t* box = cur ? d.box1 : d.box0;
+            const int* cnt = cur ? d.cnt1 : d.cnt0;
+            uint64_t* nbox = cur ? d.box0 : d.box1;
+            int* ncnt = cur ? d.cnt0 : d.cnt1;
+            if (iter > 4 * NC + 64) {  // cannot happen (each step grows the list or finishes); never hang
+                if (t == 0) { atomicOr(overflow, 2); s_done = 1; }
+                __syncthreads();
+                break;
             }
-            __syncthreads();
-            for (int p = t; p < S; p += 256) {
-                int nc = 0;
-                if (cnt[p] > 1)
+            if (stop == 3 && s_phase != 0) return;
+            if (stop >= 64 && iter == (stop - 64) % 8) return;
+            mark(8 + 4 * iter);
+            if (s_phase == 0) {
+                // ---------------- full pass (:605-664): divide every node holding more than one key
+                for (int i = t; i < 4 * S; i += kOctThreads) d.cnt4[i] = 0;
+                if (t == 0) s_nexp = 0;
+                __syncthreads();
+                // 4 candidates per step so their LDS chains overlap; few counters: aggregate per wave
+                for (int k0 = 0; k0 < K; k0 += 4 * kOctThreads) {
+                    int b[4];
+                    bool a[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kOctThreads + t;
+                        b[u] = 0;
+                        a[u] = false;
+                        if (k < K) {
+                            const int p = kn[k];
+                            a[u] = cnt[p] > 1;
+                            b[u] = 4 * p + quad_of(kd[k], box[p]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (4 * S <= 64) wave_bin_add(d.cnt4, b[u], a[u]);
+                        else if (a[u]) atomicAdd(&d.cnt4[b[u]], 1);
+                    }
+                }
+                __syncthreads();
+                mark(9 + 4 * iter);
+                for (int p = t; p < S; p += kOctThreads) {
+                    int nc = 0;
+                    if (cnt[p] > 1)
+                        for (int q = 0; q < 4; ++q) nc += d.cnt4[4 * p + q] > 0;
+                    d.sa[p] = nc;
+                    d.sb[p] = cnt[p] == 1;
+                }
+                __syncthreads();
+                const int Cn = block_excl_scan(d.sa, S, scan_tmp);
+                const int Kk = block_excl_scan(d.sb, S, scan_tmp);
+                mark(10 + 4 * iter);
+                int nexp = 0;
+                bool ovf = false;
+                for (int p = t; p < S; p += kOctThreads) {
+                    if (cnt[p] > 1) {
+                        int c = d.sa[p];
+                        for (int q = 0; q < 4; ++q) {
+                            const int n = d.cnt4[4 * p + q];
+                            if (n == 0) continue;
+                            const int np = Cn - 1 - c++;
+                            if (np < NC) {
+                                nbox[np] = child_box(box[p], q);
+                                ncnt[np] = n;
+                            } else {
+                                ovf = true;
+                            }
+                            d.cpos[4 * p + q] = np;
+                            nexp += n > 1;
+                        }
+                    } else {
+                        const int np = Cn + d.sb[p];
+                        if (np < NC) {
+                            nbox[np] = box[p];
+                            ncnt[np] = cnt[p];
+                        } else {
+                            ovf = true;
+                        }
+                        d.cpos[4 * p] = np;
+                    }
+                }
+                if (nexp) atomicAdd(&s_nexp, nexp);
+                if (ovf) atomicOr(overflow, 4);
+                __syncthreads();
+                for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {
+                    int np[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kOctThreads;
+                        if (k < K) {
+                            const int p = kn[k];
+                            np[u] = cnt[p] > 1 ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k0 + u * kOctThreads < K) kn[k0 + u * kOctThreads] = (uint16_t)np[u];
+                }
+                __syncthreads();
+                if (t == 0) {
+                    const int Sn = Cn + Kk;
+                    s_S = Sn;
+                    s_C = Cn;
+                    s_cur = nxt;
+                    if (Sn > NC) s_done = 1;
+                    else if (Sn >= N || Sn == S) s_done = 1;            // :668-671
+                    else if (Sn + 3 * s_nexp > N) s_phase = 1;          // :672
+                }
+                __syncthreads();
+            } else {
+                // ---------------- careful phase (:675-736): divide the largest nodes of the last step first
+                for (int i = t; i < 4 * C; i += kOctThreads) d.cnt4[i] = 0;
+                for (int p = t; p < S; p += kOctThreads) d.proc[p] = 0;
+                if (t == 0) s_P = 0x7fffffff;
+                __syncthreads();
+                for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {
+                    int b[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kOctThreads;
+                        b[u] = -1;
+                        if (k < K) {
+                            const int p = kn[k];
+                            if (p < C && cnt[p] > 1) b[u] = 4 * p + quad_of(kd[k], box[p]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (b[u] >= 0) atomicAdd(&d.cnt4[b[u]], 1);
+                }
+                for (int p = t; p < C; p += kOctThreads) d.sa[p] = cnt[p] > 1;
+                __syncthreads();
+                const int M = block_excl_scan(d.sa, C, scan_tmp);
+                for (int p = t; p < C; p += kOctThreads)
+                    if (cnt[p] > 1)  // size desc, then creation desc (= list position asc)
+                        d.srt[d.sa[p]] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
+                __syncthreads();
+                // rank sort, descending (size, then creation desc = position asc); the keys are unique, so
+                // rank = number of greater keys; ranks go through d.sd, then srt is rewritten as rank -> p
+                for (int i = t; i < M; i += kOctThreads) {
+                    const uint64_t v = d.srt[i];
+                    int r = 0;
+#pragma unroll 8
+                    for (int j = 0; j < M; ++j) r += d.srt[j] > v;
+                    d.sd[i] = r;
+                }
+                __syncthreads();
+                int* sp = (int*)d.srt;  // aliases srt[0 .. M/2): every srt read is behind the barriers
+                for (int i = t; i < M; i += kOctThreads) d.sb[i] = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[i] & 0xFFFFFFFFu));
+                __syncthreads();
+                for (int i = t; i < M; i += kOctThreads) sp[d.sd[i]] = d.sb[i];
+                __syncthreads();
+                // sorted candidate j -> position p, children count, running list size
+                for (int j = t; j < M; j += kOctThreads) {
+                    const int p = sp[j];
+                    int nc = 0;
                     for (int q = 0; q < 4; ++q) nc += d.cnt4[4 * p + q] > 0;
-                d.sa[p] = nc;
-                d.sb[p] = cnt[p] == 1;
-            }
-            __syncthreads();
-            const int Cn = block_excl_scan(d.sa, S, scan_tmp);
-            const int Kk = block_excl_scan(d.sb, S, scan_tmp);
-            int nexp = 0;
-            bool ovf = false;
-            for (int p = t; p < S; p += 256) {
-                if (cnt[p] > 1) {
-                    int c = d.sa[p];
+                    d.sb[j] = nc - 1;
+                    d.sd[j] = nc;
+                }
+                __syncthreads();
+                block_excl_scan(d.sb, M, scan_tmp);
+                for (int j = t; j < M; j += kOctThreads)
+                    if (S + d.sb[j] + d.sd[j] - 1 >= N) atomicMin(&s_P, j);  // :729-730 break
+                __syncthreads();
+                mark(9 + 4 * iter);
+                const int P = s_P == 0x7fffffff ? M : s_P + 1;
+                for (int j = t; j < M; j += kOctThreads) {
+                    if (j >= P) d.sd[j] = 0;
+                    else {
+                        const int p = sp[j];
+                        d.proc[p] = 1;
+                    }
+                }
+                __syncthreads();
+                const int Cn = block_excl_scan(d.sd, M, scan_tmp);
+                for (int p = t; p < S; p += kOctThreads) d.sa[p] = d.proc[p] == 0;
+                __syncthreads();
+                const int Kk = block_excl_scan(d.sa, S, scan_tmp);
+                mark(10 + 4 * iter);
+                bool ovf = false;
+                for (int j = t; j < P; j += kOctThreads) {
+                    const int p = sp[j];
+                    int c = d.sd[j];
                     for (int q = 0; q < 4; ++q) {
                         const int n = d.cnt4[4 * p + q];
                         if (n == 0) continue;
@@ -633,10 +849,11 @@ __global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict
                             ovf = true;
                         }
                         d.cpos[4 * p + q] = np;
-                        nexp += n > 1;
                     }
-                } else {
-                    const int np = Cn + d.sb[p];
+                }
+                for (int p = t; p < S; p += kOctThreads) {
+                    if (d.proc[p]) continue;
+                    const int np = Cn + d.sa[p];
                     if (np < NC) {
                         nbox[np] = box[p];
                         ncnt[np] = cnt[p];
@@ -645,152 +862,57 @@ __global__ __launch_bounds__(256) void k_octree(Geo g, const CellGeo* __restrict
                     }
                     d.cpos[4 * p] = np;
                 }
-            }
-            if (nexp) atomicAdd(&s_nexp, nexp);
-            if (ovf) atomicOr(overflow, 4);
-            __syncthreads();
-            for (int k = t; k < K; k += 256) {
-                const int p = kn[k];
-                kn[k] = (uint16_t)(cnt[p] > 1 ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p]);
-            }
-            __syncthreads();
-            if (t == 0) {
-                const int Sn = Cn + Kk;
-                s_S = Sn;
-                s_C = Cn;
-                s_cur = nxt;
-                if (Sn > NC) s_done = 1;
-                else if (Sn >= N || Sn == S) s_done = 1;            // :668-671
-                else if (Sn + 3 * s_nexp > N) s_phase = 1;          // :672
-            }
-            __syncthreads();
-        } else {
-            // ---------------- careful phase (:675-736): divide the largest nodes of the last step first
-            for (int i = t; i < 4 * C; i += 256) d.cnt4[i] = 0;
-            for (int p = t; p < S; p += 256) d.proc[p] = 0;
-            if (t == 0) s_P = 0x7fffffff;
-            __syncthreads();
-            for (int k = t; k < K; k += 256) {
-                const int p = kn[k];
-                if (p < C && cnt[p] > 1) atomicAdd(&d.cnt4[4 * p + quad_of(kd[k], box[p])], 1);
-            }
-            for (int p = t; p < C; p += 256) d.sa[p] = cnt[p] > 1;
-            __syncthreads();
-            const int M = block_excl_scan(d.sa, C, scan_tmp);
-            int m2 = 1;
-            while (m2 < M) m2 <<= 1;
-            for (int p = t; p < C; p += 256)
-                if (cnt[p] > 1)  // size desc, then creation desc (= list position asc)
-                    d.srt[d.sa[p]] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
-            for (int j = M + t; j < m2; j += 256) d.srt[j] = 0;
-            __syncthreads();
-            for (int k2 = 2; k2 <= m2; k2 <<= 1) {  // bitonic sort, descending
-                for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-                    for (int i = t; i < m2; i += 256) {
-                        const int ixj = i ^ j2;
-                        if (ixj > i) {
-                            const uint64_t a = d.srt[i], bb = d.srt[ixj];
-                            const bool desc = (i & k2) == 0;
-                            if (desc ? (a < bb) : (a > bb)) {
-                                d.srt[i] = bb;
-                                d.srt[ixj] = a;
-                            }
+                if (ovf) atomicOr(overflow, 8);
+                __syncthreads();
+                for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {
+                    int np[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = k0 + u * kOctThreads;
+                        if (k < K) {
+                            const int p = kn[k];
+                            np[u] = d.proc[p] ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p];
                         }
                     }
-                    __syncthreads();
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k0 + u * kOctThreads < K) kn[k0 + u * kOctThreads] = (uint16_t)np[u];
                 }
-            }
-            // sorted candidate j -> position p, children count, running list size
-            for (int j = t; j < M; j += 256) {
-                const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
-                int nc = 0;
-                for (int q = 0; q < 4; ++q) nc += d.cnt4[4 * p + q] > 0;
-                d.sb[j] = nc - 1;
-                d.sd[j] = nc;
-            }
-            __syncthreads();
-            block_excl_scan(d.sb, M, scan_tmp);
-            for (int j = t; j < M; j += 256)
-                if (S + d.sb[j] + d.sd[j] - 1 >= N) atomicMin(&s_P, j);  // :729-730 break
-            __syncthreads();
-            const int P = s_P == 0x7fffffff ? M : s_P + 1;
-            for (int j = t; j < M; j += 256) {
-                if (j >= P) d.sd[j] = 0;
-                else {
-                    const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
-                    d.proc[p] = 1;
+                __syncthreads();
+                if (t == 0) {
+                    const int Sn = Cn + Kk;
+                    s_S = Sn;
+                    s_C = Cn;
+                    s_cur = nxt;
+                    if (Sn > NC || Sn >= N || Sn == S) s_done = 1;  // :733-734
                 }
+                __syncthreads();
             }
-            __syncthreads();
-            const int Cn = block_excl_scan(d.sd, M, scan_tmp);
-            for (int p = t; p < S; p += 256) d.sa[p] = d.proc[p] == 0;
-            __syncthreads();
-            const int Kk = block_excl_scan(d.sa, S, scan_tmp);
-            bool ovf = false;
-            for (int j = t; j < P; j += 256) {
-                const int p = (int)(0xFFFFFFFFu - (uint32_t)(d.srt[j] & 0xFFFFFFFFu));
-                int c = d.sd[j];
-                for (int q = 0; q < 4; ++q) {
-                    const int n = d.cnt4[4 * p + q];
-                    if (n == 0) continue;
-                    const int np = Cn - 1 - c++;
-                    if (np < NC) {
-                        nbox[np] = child_box(box[p], q);
-                        ncnt[np] = n;
-                    } else {
-                        ovf = true;
-                    }
-                    d.cpos[4 * p + q] = np;
-                }
-            }
-            for (int p = t; p < S; p += 256) {
-                if (d.proc[p]) continue;
-                const int np = Cn + d.sa[p];
-                if (np < NC) {
-                    nbox[np] = box[p];
-                    ncnt[np] = cnt[p];
-                } else {
-                    ovf = true;
-                }
-                d.cpos[4 * p] = np;
-            }
-            if (ovf) atomicOr(overflow, 8);
-            __syncthreads();
-            for (int k = t; k < K; k += 256) {
-                const int p = kn[k];
-                kn[k] = (uint16_t)(d.proc[p] ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p]);
-            }
-            __syncthreads();
-            if (t == 0) {
-                const int Sn = Cn + Kk;
-                s_S = Sn;
-                s_C = Cn;
-                s_cur = nxt;
-                if (Sn > NC || Sn >= N || Sn == S) s_done = 1;  // :733-734
-            }
-            __syncthreads();
         }
-    }
-    // 3. keep the first maximum-response key of every node (:740-759), list order
-    const int S = min(s_S, NC);
-    uint32_t* best = (uint32_t*)d.cnt4;
-    for (int p = t; p < S; p += 256) best[p] = 0;
-    __syncthreads();
-    for (int k = t; k < K; k += 256) {
-        const int p = kn[k];
-        if (p < S) atomicMax(&best[p], (kd[k] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
-    }
-    __syncthreads();
-    for (int p = t; p < S; p += 256) {
-        const uint32_t k = 0xFFFFFFu - (best[p] & 0xFFFFFFu);
-        if (best[p] != 0u && (int)k < K) {
-            out[p] = kd[k];
-        } else {  // a node without keys cannot occur; flag instead of reading out of range
-            out[p] = 0u;
-            atomicOr(overflow, 16);
+        // 3. keep the first maximum-response key of every node (:740-759), list order
+        const int S = min(s_S, NC);
+        uint32_t* best = (uint32_t*)d.cnt4;
+        for (int p = t; p < S; p += kOctThreads) best[p] = 0;
+        __syncthreads();
+        for (int k = t; k < K; k += kOctThreads) {
+            const int p = kn[k];
+            if (p < S) atomicMax(&best[p], (kd[k] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
         }
-    }
-    if (t == 0) lvl_count[img * g.nlevels + l] = S;
+        __syncthreads();
+        for (int p = t; p < S; p += kOctThreads) {
+            const uint32_t k = 0xFFFFFFu - (best[p] & 0xFFFFFFu);
+            if (best[p] != 0u && (int)k < K) {
+                out[p] = kd[k];
+            } else {  // a node without keys cannot occur; flag instead of reading out of range
+                out[p] = 0u;
+                atomicOr(overflow, 16);
+            }
+        }
+        if (t == 0) lvl_count[img * g.nlevels + l] = S;
+        mark(63);
+    };
+    if (K <= kOctKeys) run(std::true_type{});
+    else run(std::false_type{});
 }
 
 // ------------------------------------------------------------------------------- descriptor math
@@ -1459,15 +1581,20 @@ size_t octree_lds_bytes(const Geo& g, int maxcell) {
     const int NC = g.max_ncap;
     int pow2 = 1;
     while (pow2 < NC) pow2 <<= 1;
-    return (size_t)8 * NC * 2 + 8 * pow2 + 4 * NC * 2 + 16 * NC * 2 + 4 * NC * 4 + 4 * (maxcell + 1);
+    return (size_t)8 * NC * 2 + 8 * pow2 + 4 * NC * 2 + 16 * NC + 8 * NC + 4 * NC * 4 + 4 * ((maxcell + 4) & ~3) +
+           6 * kOctKeys;
 }
 
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
                          uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
-                         hipStream_t s) {
+                         hipStream_t s, int variant, long long* prof) {
     const size_t lds = octree_lds_bytes(g, maxcell);
-    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, n_images), dim3(256), lds, s, g, cells, cell_count, slots, kd, kn,
-                       lvl_kp, lvl_count, overflow, maxcell);
+    if (lds > 64 * 1024) {  // gfx950: up to 160 KiB per workgroup, above 64 KiB on request
+        const hipError_t e = hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_octree, dim3(n_images, g.nlevels), dim3(kOctThreads), lds, s, g, cells, cell_count, slots, kd, kn,
+                       lvl_kp, lvl_count, overflow, maxcell, variant, prof);
     return hipGetLastError();
 }
 

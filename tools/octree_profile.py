@@ -1,0 +1,41 @@
+"""Per-phase octree timing from orbfe_debug_octree_profile (development aid): median over images of the
+wall-clock deltas (us) between marks, per level.  usage: python tools/octree_profile.py [--pairs 64]"""
+import argparse
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=64)
+    a = ap.parse_args()
+    import torch
+    from pyorbslam_amd import synth
+    from pyorbslam_amd.batch import StereoFrontEnd
+    from pyorbslam_amd._lib import call
+    imgs = torch.from_numpy(synth.make_batch(a.pairs)).cuda()
+    fe = StereoFrontEnd(max_pairs=a.pairs)
+    fe.enqueue(imgs)
+    torch.cuda.synchronize()
+    n = 2 * a.pairs * 8 * 64
+    buf = np.zeros(n, np.int64)
+    call("orbfe_debug_octree_profile", fe.handle, buf.ctypes.data_as(C.c_void_p), n)
+    m = buf.reshape(2 * a.pairs, 8, 64).astype(np.float64) / 100.0  # us
+    t0 = m[:, :, 0:1]
+    for l in range(8):
+        ids = [i for i in range(64) if (m[:, l, i] > 0).all()]
+        rel = {i: float(np.median(m[:, l, i] - m[:, l, 0])) for i in ids}
+        print(f"level {l}: " + " ".join(f"{i}:{v:.1f}" for i, v in rel.items()))
+    start = m[:, :, 0]
+    end = m[:, :, 63]
+    print("block start spread (us):", float(start.max() - start.min()), " last end - first start:",
+          float(end.max() - start.min()))
+
+
+if __name__ == "__main__":
+    main()
