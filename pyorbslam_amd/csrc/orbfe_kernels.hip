@@ -307,6 +307,8 @@ __device__ __forceinline__ uint32_t fast_m_pair(const uint32_t* R) {
 
 __device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
 
+constexpr int kFdCells = 4;  // cells per k_detect wavefront (the next cell's ROI loads overlap this one)
+
 __device__ __forceinline__ int lanes_below(uint64_t b) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
 }
@@ -324,138 +326,158 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     uint16_t* mm = roi + RP * g.max_rh;                        // (max_wh + 2) x MP: window px (x, y) at (y + 1) * MP + x + 2
     uint16_t* pq = mm + MP * (g.max_wh + 2);                   // pair queue: (y << 6) | x
     uint16_t* nq = pq + g.max_win;                             // NMS queue: (y << 6) | x
-    const int c = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
-    const CellGeo cg = cells[c];
-    int stride;
-    const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
-    const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
-    const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
-    // ---- 1. stage the ROI (16 lanes per row, 4 rows per step; up to 16 steps = 64 rows)
-    {
-        const int d = lane & 15, r0 = lane >> 4;
-        const int ndw = (rw + 4) >> 2;  // columns -1 .. rw-1
-        uint32_t lo[16], hi[16];
-        int sh[16];
+    const int img = blockIdx.y, lane = threadIdx.x;
+    const int c_first = blockIdx.x * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
+    // ROI staging, 16 lanes per row (dword d), 4 rows per step (up to 16 steps = 64 rows): each slot is
+    // one buffer_load_dwordx2 from the 4-byte aligned start of column -1, re-aligned with v_alignbyte.
+    // The loads of the next cell are issued before this cell's compute (prefetch into registers).
+    const int d = lane & 15, r0 = lane >> 4;
+    uint2 raw[16];
+    auto issue = [&](int c) {
+        const CellGeo cg = cells[c];
+        int stride;
+        const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(lvl);
+        const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0, ndw = (rw + 4) >> 2;  // columns -1 .. rw-1
+        const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
+        const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int r = r0 + 4 * k;
-            lo[k] = hi[k] = 0;
-            sh[k] = 0;
+            raw[k] = uint2{0u, 0u};
             if (r < rh && d < ndw) {
-                const uintptr_t a = (uintptr_t)(lvl + (int64_t)(cg.y0 + r) * stride + cg.x0 - 1);
-                const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
-                sh[k] = (int)(a & 3);
-                lo[k] = p[d];
-                hi[k] = p[d + 1];
+                const uint32_t off = off0 + (uint32_t)(4 * k * stride);
+                const uint32_t al = off - ((lvl_lo + off) & 3u);
+                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al + 4u * d, 0, 0));
             }
         }
+    };
+    if (c_first < c_last) issue(c_first);
+    for (int c = c_first; c < c_last; ++c) {
+        const CellGeo cg = cells[c];
+        const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
+        const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
+        {
+            int stride;
+            const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
+            const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
+            const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
+            const int ndw = (rw + 4) >> 2;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int r = r0 + 4 * k;
-            if (r < rh && d < ndw) {
-                const uint32_t w = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
-                uint2 u;
-                u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04010400u);
-                u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04030402u);
-                *(uint2*)(roi + r * RP + 4 * d) = u;
+            for (int k = 0; k < 16; ++k) {
+                const int r = r0 + 4 * k;
+                if (r < rh && d < ndw) {
+                    const int sh = (int)((lvl_lo + off0 + (uint32_t)(4 * k * stride)) & 3u);
+                    const uint32_t w = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh);
+                    uint2 u;
+                    u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04010400u);
+                    u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04030402u);
+                    *(uint2*)(roi + r * RP + 4 * d) = u;
+                }
+            }
+            // the M map with its zero border
+            uint4* m128 = (uint4*)mm;
+            const uint4 z = uint4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};
+            for (int i = lane; i < (MP / 8) * (wh + 2); i += 64) m128[i] = z;
+        }
+        if (c + 1 < c_last) issue(c + 1);  // in flight during this cell's compute
+        __syncthreads();
+        auto process = [&]() {
+            if (V == 1) {  // ablation: ROI staging only
+                if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = roi[rw * rh / 2] & 0;
+                return;
+            }
+            if (ww <= 0 || wh <= 0) {
+                if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = 0;
+                return;
+            }
+        const int tq = min(g.ini_th, g.min_th);
+        // ---- 2. pre-test of every pair (row-major: lane -> pair i = i0 + lane)
+        const int prow = (ww + 1) >> 1, npair = prow * wh;
+        const int step_y = 64 / prow, step_x = 64 - step_y * prow;
+        int npq = 0;
+        {
+            int py = lane / prow, px = lane - (lane / prow) * prow;
+            for (int i0 = 0; i0 < npair; i0 += 64) {
+                bool cand = false;
+                if (i0 + lane < npair) {
+                    const int x = 2 * px;
+                    const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + (py + 3) * RP + x + 4));
+                    cand = pb.x > tq || (pb.y > tq && x + 1 < ww);
+                }
+                const uint64_t bal = __ballot(cand);
+                if (cand) pq[npq + lanes_below(bal)] = (uint16_t)((py << 6) | (2 * px));
+                npq += __popcll(bal);
+                py += step_y;
+                px += step_x;
+                if (px >= prow) {
+                    px -= prow;
+                    ++py;
+                }
             }
         }
-        // the M map with its zero border
-        uint32_t* m32 = (uint32_t*)mm;
-        for (int i = lane; i < (MP / 2) * (wh + 2); i += 64) m32[i] = 0x3C003C00u;
-    }
-    __syncthreads();
-    if (V == 1) {  // ablation: ROI staging only
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = roi[rw * rh / 2] & 0;
-        return;
-    }
-    if (ww <= 0 || wh <= 0) {
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = 0;
-        return;
-    }
-    const int tq = min(g.ini_th, g.min_th);
-    // ---- 2. pre-test of every pair (row-major: lane -> pair i = i0 + lane)
-    const int prow = (ww + 1) >> 1, npair = prow * wh;
-    const int step_y = 64 / prow, step_x = 64 - step_y * prow;
-    int npq = 0;
-    {
-        int py = lane / prow, px = lane - (lane / prow) * prow;
-        for (int i0 = 0; i0 < npair; i0 += 64) {
-            bool cand = false;
-            if (i0 + lane < npair) {
-                const int x = 2 * px;
-                const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + (py + 3) * RP + x + 4));
-                cand = pb.x > tq || (pb.y > tq && x + 1 < ww);
-            }
-            const uint64_t bal = __ballot(cand);
-            if (cand) pq[npq + lanes_below(bal)] = (uint16_t)((py << 6) | (2 * px));
-            npq += __popcll(bal);
-            py += step_y;
-            px += step_x;
-            if (px >= prow) {
-                px -= prow;
-                ++py;
-            }
+        __syncthreads();
+        if (V == 2) {  // ablation: + pre-test / pair queue
+            if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = npq & 0;
+            return;
         }
-    }
-    __syncthreads();
-    if (V == 2) {  // ablation: + pre-test / pair queue
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = npq & 0;
-        return;
-    }
-    // ---- 3. exact M of the queued pairs -> M map; NMS candidates -> queue
-    const int tlow = max(tq, 1);
-    int nnq = 0;
-    for (int k0 = 0; k0 < npq; k0 += 64) {
-        bool h0 = false, h1 = false;
-        uint32_t e = 0;
-        if (k0 + lane < npq) {
-            e = pq[k0 + lane];
-            const int x = e & 63, y = e >> 6;
-            uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
-            if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
-            *(uint32_t*)(mm + (y + 1) * MP + x + 2) = m;
-            h0 = (int)(m & 0x3FFu) > tlow;
-            h1 = (int)((m >> 16) & 0x3FFu) > tlow;
-        }
-        const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-        const int o = nnq + lanes_below(b0) + lanes_below(b1);
-        if (h0) nq[o] = (uint16_t)e;
-        if (h1) nq[o + (int)h0] = (uint16_t)(e + 1);
-        nnq += __popcll(b0) + __popcll(b1);
-    }
-    __syncthreads();
-    if (V == 3) {  // ablation: + exact M
-        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
-        return;
-    }
-    // ---- 4. NMS (local max) over the queue + ordered compaction at iniTh, else minTh
-    uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-    int total = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        const int thb = 0x3C00 + max(pass == 0 ? g.ini_th : g.min_th, 1);
-        total = 0;
-        for (int k0 = 0; k0 < nnq; k0 += 64) {
-            bool keep = false;
-            int e = 0, own = 0;
-            if (k0 + lane < nnq) {
-                e = nq[k0 + lane];
-                const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
-                own = q[0];
-                const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]), imax3(q[MP - 1], q[MP], q[MP + 1]));
-                keep = own > max(imax3(nmax, q[-1], q[1]), thb);
+        // ---- 3. exact M of the queued pairs -> M map; NMS candidates -> queue
+        const int tlow = max(tq, 1);
+        int nnq = 0;
+        for (int k0 = 0; k0 < npq; k0 += 64) {
+            bool h0 = false, h1 = false;
+            uint32_t e = 0;
+            if (k0 + lane < npq) {
+                e = pq[k0 + lane];
+                const int x = e & 63, y = e >> 6;
+                uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
+                if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
+                *(uint32_t*)(mm + (y + 1) * MP + x + 2) = m;
+                h0 = (int)(m & 0x3FFu) > tlow;
+                h1 = (int)((m >> 16) & 0x3FFu) > tlow;
             }
-            const uint64_t bal = __ballot(keep);
-            const int o = total + lanes_below(bal);
-            // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-            if (keep && o < cg.slot_cap)
-                out[o] = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
-                         ((uint32_t)((own & 0xFF) - 1) << 24);
-            total += __popcll(bal);
+            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+            const int o = nnq + lanes_below(b0) + lanes_below(b1);
+            if (h0) nq[o] = (uint16_t)e;
+            if (h1) nq[o + (int)h0] = (uint16_t)(e + 1);
+            nnq += __popcll(b0) + __popcll(b1);
         }
-        if (total > 0 || g.min_th == g.ini_th) break;
+        __syncthreads();
+        if (V == 3) {  // ablation: + exact M
+            if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
+            return;
+        }
+        // ---- 4. NMS (local max) over the queue + ordered compaction at iniTh, else minTh
+        uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
+        int total = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            const int thb = 0x3C00 + max(pass == 0 ? g.ini_th : g.min_th, 1);
+            total = 0;
+            for (int k0 = 0; k0 < nnq; k0 += 64) {
+                bool keep = false;
+                int e = 0, own = 0;
+                if (k0 + lane < nnq) {
+                    e = nq[k0 + lane];
+                    const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
+                    own = q[0];
+                    const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]), imax3(q[MP - 1], q[MP], q[MP + 1]));
+                    keep = own > max(imax3(nmax, q[-1], q[1]), thb);
+                }
+                const uint64_t bal = __ballot(keep);
+                const int o = total + lanes_below(bal);
+                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+                if (keep && o < cg.slot_cap)
+                    out[o] = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
+                             ((uint32_t)((own & 0xFF) - 1) << 24);
+                total += __popcll(bal);
+            }
+            if (total > 0 || g.min_th == g.ini_th) break;
+        }
+        if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
+        };
+        process();
+        __syncthreads();  // the next cell overwrites the ROI and the M map
     }
-    if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
 }
 
 // ------------------------------------------------------------------------------- k_octree
@@ -1561,7 +1583,7 @@ template <int RP>
 static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                              int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
     const size_t lds = detect_lds_bytes(g);
-    const dim3 grid(g.ncells, n_images), blk(64);
+    const dim3 grid((g.ncells + kFdCells - 1) / kFdCells, n_images), blk(64);
     auto k = variant == 1 ? k_detect<1, RP> : variant == 2 ? k_detect<2, RP> : variant == 3 ? k_detect<3, RP>
                                                                                            : k_detect<0, RP>;
     hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
