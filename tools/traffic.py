@@ -1,0 +1,55 @@
+"""HBM traffic per bench step and stage from rocprofv3 --pmc runs of bench.py (FETCH_SIZE and WRITE_SIZE
+in separate passes, as MI355X_MICROARCH.md prescribes).  FETCH_SIZE / WRITE_SIZE are in KiB per
+dispatch; FETCH_SIZE is doubled (gfx950 tallies 128-B memory-side read requests at 64 B).  These
+kernels use dword/dwordx2/byte loads, for which the guide's x2 calibration is not established, so the
+raw and corrected values are both kept.
+usage: python tools/traffic.py PMC_DIR WORKLOAD OUT_JSON [steps]"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+STAGES = {"resize": ["k_resize"], "detect": ["k_detect"], "octree": ["k_octree"],
+          "describe": ["k_blur", "k_describe"], "stereo": ["k_stereo_bucket", "k_stereo"]}
+
+
+def per_kernel(d, counter):
+    acc = collections.defaultdict(list)
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("orbfe::", "")
+                acc[name].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    d, workload, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    fetch, write = per_kernel(d, "FETCH_SIZE"), per_kernel(d, "WRITE_SIZE")
+    res = {}
+    for st, ks in STAGES.items():
+        # bytes per step: all dispatches of the stage's kernels / number of steps (dispatches of the
+        # first kernel / its launches per step)
+        per_step_launches = 7 if st == "resize" else 1
+        nsteps = len(fetch.get(ks[0], [])) / per_step_launches
+        if not nsteps:
+            continue
+        f = sum(sum(fetch.get(k, [])) for k in ks) / nsteps
+        w = sum(sum(write.get(k, [])) for k in ks) / nsteps
+        res[st] = {"fetch_raw_bytes": f, "write_bytes": w, "bytes": 2 * f + w, "steps_seen": nsteps}
+    data = {}
+    try:
+        data = json.load(open(out))
+    except Exception:
+        pass
+    data[workload] = {st: v["bytes"] for st, v in res.items()}
+    data[workload + "_detail"] = res
+    json.dump(data, open(out, "w"), indent=1, sort_keys=True)
+    for st, v in res.items():
+        print(f"{st:9s} fetch(raw) {v['fetch_raw_bytes'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB  "
+              f"corrected total {v['bytes'] / 1e6:9.1f} MB per step")
+
+
+if __name__ == "__main__":
+    main()
