@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--cpu-sample", type=int, default=24, help="pairs timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="pairs timed for cpu_baseline (0 = skip; 64 is about 15 s)")
     ap.add_argument("--check", action="store_true", help="verify the last step's pair 0 against the oracle")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather every pair's results on rank 0 (dist.gather_results, untimed)")
