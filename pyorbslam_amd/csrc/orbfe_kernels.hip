@@ -1302,14 +1302,6 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
 }
 
 // ------------------------------------------------------------------------------- k_stereo
-__device__ __forceinline__ int sheared_px(const uint8_t* lvl, int stride, int w, int h, int r, int c) {
-    // GetImagePyramid's caster reads the padded level's ROI pointer with a contiguous stride of w
-    const int pw = w + 2 * kEdge;
-    const int f = kEdge * pw + kEdge + r * w + c;
-    const int pr = f / pw, pc = f - pr * pw;
-    return lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)];
-}
-
 __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Python round(): half to even
 
 // Row buckets of the right keypoints (Frame.py:170-179): right keypoint iR is listed in every row of
@@ -1352,19 +1344,50 @@ __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
     }
 }
 
-// One wavefront per left keypoint (Frame.py:186-278).
+// Four left keypoints per wavefront, 16 lanes each (Frame.py:186-278); row q = lane >> 4 of the wave.
 //  search: the row bucket of int(vL); gates |octR - octL| <= 1 and uL - maxD <= uR <= uL; Hamming
-//          distance by 8 popcounts; (distance, iR) lexicographic wave minimum; accept if < 75
-//          (TH_HIGH start 100, thOrbDist = (TH_HIGH + TH_LOW) / 2).
-//  refine: the 11 x 11 left patch and the 11 x 21 right strip of the *sheared* pyramid views are
-//          staged in LDS (one index division per staged pixel), 11 shifts x 11 rows of SAD sums, first
-//          minimum, parabola and depth in IEEE float32 like the NumPy-2 chain of the reference.
+//          distance by 8 popcounts; (distance, iR) lexicographic minimum as one u32 (distance << 16 | iR)
+//          reduced by DPP over the 16-lane row; accept if < 75 (TH_HIGH start 100,
+//          thOrbDist = (TH_HIGH + TH_LOW) / 2).
+//  refine: the 11 x 11 left patch and the 11 x 21 right strip of the *sheared* pyramid views are staged
+//          in LDS one row per lane (one index division per row: consecutive sheared pixels advance
+//          linearly and wrap at most once), 11 shifts x 11 rows of SAD sums, first minimum, parabola and
+//          depth in IEEE float32 like the NumPy-2 chain of the reference.
+__device__ __forceinline__ uint32_t row16_min(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+    return v;
+}
+
+// n consecutive pixels (row r, columns c0 ..) of the sheared view of a level -> dst
+__device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
+                                            uint8_t* dst) {
+    const int pw = w + 2 * kEdge;
+    const int f = kEdge * pw + kEdge + r * w + c0;
+    int pr = f / pw, pc = f - pr * pw;
+    uint8_t v[21];
+#pragma unroll
+    for (int j = 0; j < 21; ++j) {
+        if (j < n) v[j] = lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)];
+        if (++pc == pw) {
+            pc = 0;
+            ++pr;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 21; ++j)
+        if (j < n) dst[j] = v[j];
+}
+
 __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
-    __shared__ int sad[4][11];
-    __shared__ uint8_t sL[4][121];
-    __shared__ uint8_t sR[4][231];
-    const int pr = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int iL = blockIdx.x * 4 + w;
+    __shared__ int sad[16][11];
+    __shared__ uint8_t sL[16][121];
+    __shared__ uint8_t sR[16][231];
+    const int pr = blockIdx.y, lane = threadIdx.x & 63, sl = lane & 15;
+    const int kq = threadIdx.x >> 4;  // keypoint of this 16-lane group inside the block
+    const int iL = blockIdx.x * 16 + kq;
     const int nL = A.countL[pr * A.cnt_stride];
     const bool active = iL < nL;
     const orbfe_keypoint* KL = A.kpsL + pr * A.kp_stride;
@@ -1372,9 +1395,9 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     const uint8_t* DL = A.descL + pr * A.kp_stride * 32;
     const uint8_t* DR = A.descR + pr * A.kp_stride * 32;
     const float2* rinfo = A.rinfo + pr * A.out_stride;
-    if (lane < 11) sad[w][lane] = 0;
-    int best = 256, bidx = 0x7fffffff;
-    orbfe_keypoint kl;
+    if (sl < 11) sad[kq][sl] = 0;
+    uint32_t key = 0xFFFFFFFFu;  // (distance << 16) | iR
+    orbfe_keypoint kl = {};
     if (active) {
         kl = KL[iL];
         const int row = min((int)(double)kl.y, g.H - 1);
@@ -1384,7 +1407,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         const float minU = __fsub_rn(kl.x, A.maxD);
         const uint4* dl4 = (const uint4*)(DL + (int64_t)iL * 32);
         const uint4 a0 = dl4[0], a1 = dl4[1];
-        for (int k = b + lane; k < e; k += 64) {
+        for (int k = b + sl; k < e; k += 16) {
             const int iR = bidxs[k];
             const float2 ri = rinfo[iR];
             const int oct = __float_as_int(ri.y);
@@ -1392,37 +1415,28 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             if (!(minU <= ri.x && (double)ri.x <= (double)kl.x)) continue;
             const uint4* dr4 = (const uint4*)(DR + (int64_t)iR * 32);
             const uint4 b0 = dr4[0], b1 = dr4[1];
-            const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-                             __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-            if (dist < best || (dist == best && iR < bidx)) {
-                best = dist;
-                bidx = iR;
-            }
+            const uint32_t dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                                  __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+            key = min(key, (dist << 16) | (uint32_t)iR);
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bidx, o, 64);
-        if (ob < best || (ob == best && oi < bidx)) {
-            best = ob;
-            bidx = oi;
-        }
-    }
+    key = row16_min(key);
+    const int best = (int)(key >> 16), bidx = (int)(key & 0xFFFFu);
     int status = 0;
     float uR = -1.f, depth = -1.f;
     const bool refine = active && best < 75;  // TH_HIGH start, thOrbDist = 75 (:166, :203, :222)
-    int scaleduR0 = 0, scaledvL = 0, scaleduL = 0, lw = 0, lh = 0, lstride = 0;
-    const uint8_t *lvlL = nullptr, *lvlR = nullptr;
+    int scaleduR0 = 0;
     bool do_sad = false;
     if (refine) {
         const int oct = kl.octave;
         const double isf = (double)g.inv_scale[oct];
         const float uR0 = KR[bidx].x;
-        scaleduL = (int)py_round((double)kl.x * isf);
-        scaledvL = (int)py_round((double)kl.y * isf);
+        const int scaleduL = (int)py_round((double)kl.x * isf);
+        const int scaledvL = (int)py_round((double)kl.y * isf);
         scaleduR0 = (int)py_round((double)uR0 * isf);
-        lw = g.lv[oct].w;
-        lh = g.lv[oct].h;
+        const int lw = g.lv[oct].w, lh = g.lv[oct].h;
+        const uint8_t *lvlL, *lvlR;
+        int lstride;
         if (oct == 0) {
             lvlL = A.lvl0L + pr * A.lvl0_stride;
             lvlR = A.lvl0R + pr * A.lvl0_stride;
@@ -1435,43 +1449,37 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
                  scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
-        if (do_sad) {
-            for (int i = lane; i < 121; i += 64) {
-                const int r = i / 11, c = i - r * 11;
-                sL[w][i] = (uint8_t)sheared_px(lvlL, lstride, lw, lh, scaledvL - 5 + r, scaleduL - 5 + c);
-            }
-            for (int i = lane; i < 231; i += 64) {
-                const int r = i / 21, c = i - r * 21;
-                sR[w][i] = (uint8_t)sheared_px(lvlR, lstride, lw, lh, scaledvL - 5 + r, scaleduR0 - 10 + c);
-            }
+        if (do_sad && sl < 11) {
+            sheared_row(lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, &sL[kq][sl * 11]);
+            sheared_row(lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, &sR[kq][sl * 21]);
         }
     }
     __syncthreads();
     if (do_sad) {
-        const int lc = sL[w][60];  // IL[5][5]
+        const int lc = sL[kq][60];  // IL[5][5]
         // 11 shifts x 11 rows = 121 row sums of 11 |(IL - IL[5,5]) - (IR - IR[5,5])| terms
-        for (int it = lane; it < 121; it += 64) {
+        for (int it = sl; it < 121; it += 16) {
             const int s = it / 11, r = it - s * 11;
-            const int rc = sR[w][5 * 21 + s + 5];
+            const int rc = sR[kq][5 * 21 + s + 5];
             int acc = 0;
 #pragma unroll
             for (int c = 0; c < 11; ++c) {
-                const int dd = (sL[w][r * 11 + c] - lc) - (sR[w][r * 21 + s + c] - rc);
+                const int dd = (sL[kq][r * 11 + c] - lc) - (sR[kq][r * 21 + s + c] - rc);
                 acc += dd < 0 ? -dd : dd;
             }
-            atomicAdd(&sad[w][s], acc);
+            atomicAdd(&sad[kq][s], acc);
         }
     }
     __syncthreads();
-    if (do_sad && lane == 0) {
-        int bi = 0, bd = sad[w][0];
+    if (do_sad && sl == 0) {
+        int bi = 0, bd = sad[kq][0];
         for (int s = 1; s < 11; ++s)
-            if (sad[w][s] < bd) {
-                bd = sad[w][s];
+            if (sad[kq][s] < bd) {
+                bd = sad[kq][s];
                 bi = s;
             }
         if (bi != 0 && bi != 10) {
-            const int d1 = sad[w][bi - 1], d2 = sad[w][bi], d3 = sad[w][bi + 1];
+            const int d1 = sad[kq][bi - 1], d2 = sad[kq][bi], d3 = sad[kq][bi + 1];
             const float deltaR = __fdiv_rn((float)(d1 - d3), (float)(2 * (d1 + d3 - 2 * d2)));
             if (!(deltaR < -1.f || deltaR > 1.f)) {
                 const float bestuR = __fmul_rn(g.scale[kl.octave], __fadd_rn((float)(scaleduR0 + bi - 5), deltaR));
@@ -1490,7 +1498,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             }
         }
     }
-    if (active && lane == 0) {
+    if (active && sl == 0) {
         const int64_t o = pr * A.out_stride + iL;
         A.u_right[o] = status ? uR : -1.f;
         A.depth[o] = status ? depth : -1.f;
@@ -1638,7 +1646,7 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
 
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
     hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);
-    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 3) / 4, n_pairs), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 15) / 16, n_pairs), dim3(256), 0, s, g, a);
     return hipGetLastError();
 }
 

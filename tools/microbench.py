@@ -11,7 +11,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pairs", type=int, default=64)
+    ap.add_argument("--pairs", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("items", nargs="*", default=["0:0", "1:0", "2:0", "3:0", "4:0"])
