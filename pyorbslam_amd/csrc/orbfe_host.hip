@@ -100,6 +100,7 @@ struct orbfe_ctx {
 
     DevBuf<CellGeo> d_cells;
     DevBuf<ResizeX> d_xt;
+    DevBuf<uint32_t> d_mw;  // k_describe: [4 row shifts][31 x 9 window dwords] (disc byte mask, m10 weights)
     DevBuf<ResizeY> d_yt;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
@@ -131,6 +132,10 @@ struct orbfe_ctx {
     bool prof_on = false;
 
     hipStream_t own_stream = nullptr;
+    // k_blur runs on a side stream concurrently with k_detect / k_octree (fork after the pyramid, join
+    // before k_describe); events only, so the batch stays capturable into a HIP graph
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t last_stream = nullptr;
     const uint8_t* last_in = nullptr;  // device input of the last extraction
     int64_t last_pitch = 0;
@@ -142,6 +147,9 @@ struct orbfe_ctx {
     ~orbfe_ctx() {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
+        if (side_stream) (void)hipStreamDestroy(side_stream);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
     }
 };
 
@@ -387,6 +395,22 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
         HIPCK(hipMemcpy(c.d_cells.p, c.cells.data(), c.cells.size() * sizeof(CellGeo), hipMemcpyHostToDevice));
+        {   // centroid masks/weights of k_describe, a function of umax only
+            std::vector<uint32_t> mw(4 * 31 * 9 * 2);
+            for (int sh = 0; sh < 4; ++sh)
+                for (int slot = 0; slot < 31 * 9; ++slot) {
+                    const int r = slot / 9, d = slot % 9, v = r - kHalfPatch, um = c.umax[v < 0 ? -v : v];
+                    const int u0 = 4 * d - sh - kHalfPatch;
+                    const int blo = std::min(std::max(-um - u0, 0), 4), bhi = std::min(std::max(um - u0 + 1, 0), 4);
+                    const int n = bhi - blo;
+                    const uint32_t mask = n > 0 ? (0xFFFFFFFFu >> (32 - 8 * n)) << (8 * blo) : 0u;
+                    const uint32_t w = (uint32_t)(u0 + 18) * 0x01010101u + 0x03020100u;  // byte weights u0 + 18 + b
+                    mw[2 * (sh * 279 + slot)] = mask;
+                    mw[2 * (sh * 279 + slot) + 1] = w;
+                }
+            c.d_mw.ensure(mw.size());
+            HIPCK(hipMemcpy(c.d_mw.p, mw.data(), mw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
         c.d_xt.ensure(c.xt.size());
         if (!c.xt.empty())
             HIPCK(hipMemcpy(c.d_xt.p, c.xt.data(), c.xt.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
@@ -440,15 +464,26 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     for (int l = 1; l < g.nlevels; ++l)
         HIPCK(launch_resize(g, l, d_in, pitch, c.d_ws.p, c.d_xt.p, c.d_yt.p, n, s));
     prof_mark(c, s, 1);
+    // fork: the blur of every level only needs the pyramid; it overlaps FAST and the octree, which are
+    // bound by VALU/LDS issue and latency rather than memory
+    if (!c.side_stream) {
+        HIPCK(hipStreamCreateWithFlags(&c.side_stream, hipStreamNonBlocking));
+        HIPCK(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+    }
+    HIPCK(hipEventRecord(c.ev_fork, s));
+    HIPCK(hipStreamWaitEvent(c.side_stream, c.ev_fork, 0));
+    HIPCK(launch_blur(g, d_in, pitch, c.d_ws.p, c.d_blur.p, n, c.side_stream));
+    HIPCK(hipEventRecord(c.ev_join, c.side_stream));
     if (g.ncells > 0)
         HIPCK(launch_detect(g, c.d_cells.p, d_in, pitch, c.d_ws.p, c.d_cell_count.p, c.d_slots.p, n, s));
     prof_mark(c, s, 2);
     HIPCK(launch_octree(g, c.d_cells.p, c.d_cell_count.p, c.d_slots.p, c.d_kd.p, c.d_kn.p, c.d_lvl_kp.p,
                         c.d_lvl_count.p, c.d_overflow.p, c.maxcell, n, s));
     prof_mark(c, s, 3);
-    HIPCK(launch_blur(g, d_in, pitch, c.d_ws.p, c.d_blur.p, n, s));
+    HIPCK(hipStreamWaitEvent(s, c.ev_join, 0));  // join
     HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_blur.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p,
-                          c.d_count.p, n, s));
+                          c.d_count.p, c.d_mw.p, n, s));
     prof_mark(c, s, 4);
     c.last_in = d_in;
     c.last_pitch = pitch;
@@ -881,7 +916,8 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                         HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s));
                     if (variant != 1)
                         HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
-                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, n, s));
+                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_mw.p,
+                                              n, s));
                     break;
                 case 4:
                     if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");

@@ -1169,18 +1169,22 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
                                                   const uint8_t* __restrict__ ws, const uint8_t* __restrict__ blur,
                                                   const uint32_t* __restrict__ lvl_kp,
                                                   const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
-                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count) {
-    __shared__ int s_umax[16];
+                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
+                                                  const uint2* __restrict__ mw_tab) {
     __shared__ float4 s_pat[256];
+    // per (row shift sh, window slot): the byte mask of the umax disc and the dot4 weights of m10
+    __shared__ uint2 s_mw[4][31 * 9];
     // XCD-aware remap of the flattened grid: hardware block i runs on XCD i % 8
     const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
     const int per = nb >> 3;
     const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;
-    const int img = lb / gridDim.x, blk = lb - img * gridDim.x;
+    // wave-uniform: keep the image / block index (and everything derived) in SGPRs
+    const int img = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
+    const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
     const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
     const int wv = blk * kDescWaves + (threadIdx.x >> 6);
-    if (threadIdx.x < 16) s_umax[threadIdx.x] = g.umax[threadIdx.x];
     s_pat[threadIdx.x] = ((const float4*)c_pattern)[threadIdx.x];
+    for (int i = threadIdx.x; i < 4 * 31 * 9; i += 256) (&s_mw[0][0])[i] = mw_tab[i];
     // per level: keypoints (pre) and waves of 4 (wpre), wave-uniform
     const int* cnt = lvl_count + img * g.nlevels;
     int pre[kMaxLevels + 1], wpre[kMaxLevels + 1];
@@ -1212,14 +1216,19 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     const __amdgpu_buffer_rsrc_t lr = uniform_rsrc(lvl);
     const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;  // provably 24-bit: v_mul_u32_u24, full rate
     constexpr int NW = (31 * 9 + 15) / 16;
-    // slot sl + 16 k of the 31 x 9 window -> (row r, dword d), stepped without division (16 = 9 + 7)
-    int rk[NW], dk[NW];
+    // slot sl + 16 k of the 31 x 9 window -> (row r, dword d), stepped without division (16 = 9 + 7);
+    // recomputed in the second loop rather than kept live across the loads
+    const int r_init = sl >= 9 ? 1 : 0, d_init = sl - 9 * r_init;
+    uint32_t word[NW];
     {
-        int r = sl >= 9 ? 1 : 0, d = sl - 9 * r;
+        int r = r_init, d = d_init;
 #pragma unroll
         for (int k = 0; k < NW; ++k) {
-            rk[k] = r;
-            dk[k] = d;
+            word[k] = 0;
+            if (r < 31) {
+                const uint32_t off = off0 + (uint32_t)(r & 63) * stride24;  // both operands provably 24-bit
+                word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * d - (lvl_lo & 3u), 0, 0);
+            }
             d += 7;
             r += 1;
             if (d >= 9) {
@@ -1228,33 +1237,27 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
             }
         }
     }
-    uint32_t word[NW];
-#pragma unroll
-    for (int k = 0; k < NW; ++k) {
-        word[k] = 0;
-        if (rk[k] < 31) {
-            const uint32_t off = off0 + (uint32_t)rk[k] * stride24;
-            word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * dk[k] - (lvl_lo & 3u), 0, 0);
-        }
-    }
     // m10 = sum (u0 + b) val_b, m01 = sum v val_b with non-negative byte weights (u0 + 18 + b), (v + 15)
-    // accumulated by v_dot4 and corrected by -18 / -15 x sum(val)
+    // accumulated by v_dot4 and corrected by -18 / -15 x sum(val); masks and m10 weights from s_mw
     uint32_t a10 = 0, a01 = 0, a1 = 0;
+    {
+        int r = r_init, d = d_init;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) {
-        if (rk[k] < 31) {
-            const int r = rk[k], d = dk[k];
-            const int sh = (int)((lvl_lo + off0 + (uint32_t)r * stride24) & 3u);
-            const int v = r - kHalfPatch, um = s_umax[v < 0 ? -v : v];
-            const int u0 = 4 * d - sh - kHalfPatch;  // u of byte 0
-            const int blo = min(max(-um - u0, 0), 4), bhi = min(max(um - u0 + 1, 0), 4);
-            const int n = bhi - blo;
-            const uint32_t mask = n > 0 ? (0xFFFFFFFFu >> (32 - 8 * n)) << (8 * blo) : 0u;
-            const uint32_t mw = word[k] & mask;
-            // byte broadcasts by v_perm (selector 0 = byte 0 of the second source in every byte)
-            a10 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)(u0 + 18), 0u) + 0x03020100u, a10, false);
-            a01 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)(v + 15), 0u), a01, false);
-            a1 = __builtin_amdgcn_udot4(mw, 0x01010101u, a1, false);
+        for (int k = 0; k < NW; ++k) {
+            if (r < 31) {
+                const int sh = (int)((lvl_lo + off0 + (uint32_t)(r & 63) * stride24) & 3u);
+                const uint2 mw2 = (&s_mw[0][0])[sh * 279 + ((r & 63) << 3) + (r & 63) + d];
+                const uint32_t mw = word[k] & mw2.x;
+                a10 = __builtin_amdgcn_udot4(mw, mw2.y, a10, false);
+                a01 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)r, 0u), a01, false);  // v + 15 = r
+                a1 = __builtin_amdgcn_udot4(mw, 0x01010101u, a1, false);
+            }
+            d += 7;
+            r += 1;
+            if (d >= 9) {
+                d -= 9;
+                r += 1;
+            }
         }
     }
     int m10 = (int)a10 - 18 * (int)a1, m01 = (int)a01 - 15 * (int)a1;
@@ -1266,7 +1269,11 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     // ---- steered BRIEF: 32 samples per lane (|offset| <= 13 * sqrt 2 < 19), 32-bit offsets from the
     // corner (cy - 19, cx - 19), which is >= 0: detection windows start 19 pixels inside every level
     const __amdgpu_buffer_rsrc_t br = uniform_rsrc(blur + (int64_t)img * g.blur_bytes + L.blur_off);
-    const uint32_t boff0 = (uint32_t)((cy - 19) * L.pitch + cx - 19), pitch24 = (uint32_t)L.pitch & 0xFFFFFFu;
+    // rint by the 1.5 * 2^23 trick: the sum's low mantissa bits hold 0x400000 + rint(x); v_mad_u32_u24
+    // reads only the low 24 bits, and the biases fold into one per-keypoint constant (mod 2^32)
+    const uint32_t pitch24 = (uint32_t)L.pitch & 0xFFFFFFu;
+    const uint32_t boff = (uint32_t)((cy - 19) * L.pitch + cx - 19) + 19u * pitch24 + 19u - 0x400000u * pitch24 -
+                          __float_as_uint(12582912.0f);
     int val[32];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1274,10 +1281,9 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
-            const int rr = __float2int_rn(fmaf(px, b, __fmul_rn(py, a)));
-            const int cc = __float2int_rn(fmaf(px, a, -__fmul_rn(py, b)));
-            val[2 * i + e] = __builtin_amdgcn_raw_buffer_load_b8(
-                br, boff0 + ((uint32_t)(rr + 19) & 0xFFu) * pitch24 + (uint32_t)(cc + 19), 0, 0);
+            const uint32_t fr = __float_as_uint(__fadd_rn(fmaf(px, b, __fmul_rn(py, a)), 12582912.0f));
+            const uint32_t fc = __float_as_uint(__fadd_rn(fmaf(px, a, -__fmul_rn(py, b)), 12582912.0f));
+            val[2 * i + e] = __builtin_amdgcn_raw_buffer_load_b8(br, (fr & 0xFFFFFFu) * pitch24 + fc + boff, 0, 0);
         }
     }
     uint64_t mine = 0;
@@ -1636,11 +1642,11 @@ hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const 
 
 hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
                            const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
-                           int* out_count, int n_images, hipStream_t s) {
+                           int* out_count, const uint32_t* mw, int n_images, hipStream_t s) {
     int waves = 0;  // most waves an image can need: 4 keypoints per wave, per level
     for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + 3) / 4;
     hipLaunchKernelGGL(k_describe, dim3((waves + kDescWaves - 1) / kDescWaves, n_images), dim3(256), 0, s, g, in,
-                       in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count);
+                       in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, (const uint2*)mw);
     return hipGetLastError();
 }
 
