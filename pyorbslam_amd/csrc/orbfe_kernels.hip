@@ -322,7 +322,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     constexpr int S = RP / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* roi = (uint16_t*)lds;                            // max_rh rows x RP
-    const int MP = g.fd_mp;
+    const int MP = g.fd_mp & 0xFFFF;  // provably 16-bit: row offsets use v_mul_u32_u24
     uint16_t* mm = roi + RP * g.max_rh;                        // (max_wh + 2) x MP: window px (x, y) at (y + 1) * MP + x + 2
     uint16_t* pq = mm + MP * (g.max_wh + 2);                   // pair queue: (y << 6) | x
     uint16_t* nq = pq + g.max_win;                             // NMS queue: (y << 6) | x
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
                 bool cand = false;
                 if (i0 + lane < npair) {
                     const int x = 2 * px;
-                    const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + (py + 3) * RP + x + 4));
+                    const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + ((py & 63) + 3) * RP + x + 4));
                     cand = pb.x > tq || (pb.y > tq && x + 1 < ww);
                 }
                 const uint64_t bal = __ballot(cand);
