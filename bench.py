@@ -92,10 +92,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--pairs", type=int, default=128, help="stereo pairs per step per GPU")
+    ap.add_argument("--pairs", type=int, default=256, help="stereo pairs per step per GPU")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--no-prof", action="store_true", help="no per-stage HIP events (roofline omitted)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="independent front-end handles per GPU, each on its own stream with P/streams pairs")
+    ap.add_argument("--lanes", type=int, default=1, help="internal concurrent chunks per handle (orbfe_set_lanes)")
     ap.add_argument("--cpu-sample", type=int, default=64, help="pairs timed for cpu_baseline (0 = skip; 64 is about 15 s)")
     ap.add_argument("--check", action="store_true", help="verify the last step's pair 0 against the oracle")
     ap.add_argument("--gather", action="store_true",
@@ -124,19 +128,30 @@ def main():
     import ctypes as C
 
     P = args.pairs
+    S = max(1, args.streams)
+    if P % S:
+        raise SystemExit("--pairs must be a multiple of --streams")
     host = synth.make_batch(P, seed0=rank * P, width=args.width, height=args.height)
     images = torch.from_numpy(host).to(dev)
-    fe = StereoFrontEnd(args.width, args.height, max_pairs=P, nfeatures=args.nfeatures)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+    # S sub-batches of P/S pairs, each with its own handle (buffers) and stream, so that the latency-bound
+    # stages of one overlap the issue-bound stages of another; every pair is still processed exactly once
+    fes = [StereoFrontEnd(args.width, args.height, max_pairs=P // S, nfeatures=args.nfeatures, lanes=args.lanes)
+           for _ in range(S)]
+    fe = fes[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    subs = [images[2 * (P // S) * i: 2 * (P // S) * (i + 1)] for i in range(S)]
 
     def step():
-        fe.enqueue(images, P, KITTI_BF, KITTI_FX, stream_ptr=sptr)
+        for f, st, sub in zip(fes, streams, subs):
+            f.enqueue(sub, P // S, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    call("orbfe_profile_begin", fe.handle, args.steps)
+    # per-stage HIP events on handle 0's stream (its stages run concurrently with the other handles')
+    prof = not args.no_prof
+    if prof:
+        call("orbfe_profile_begin", fe.handle, args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -149,8 +164,11 @@ def main():
     elapsed = time.perf_counter() - t0
     ms = (C.c_float * 5)()
     nb = C.c_int32()
-    call("orbfe_profile_read", fe.handle, ms, C.byref(nb))
-    stage_ms = {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
+    if prof:
+        call("orbfe_profile_read", fe.handle, ms, C.byref(nb))
+        stage_ms = {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
+    else:
+        stage_ms = {}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         t = t.to(dev) if dist.get_backend() == "nccl" else t
@@ -160,8 +178,8 @@ def main():
     if args.gather and world > 1:
         from pyorbslam_amd import dist as D
         tg = time.perf_counter()
-        recs = np.stack([D.pack(fe.kp_cap, *fe.fetch_image(2 * p), *fe.fetch_image(2 * p + 1), fe.fetch_stereo(p))
-                         for p in range(P)])
+        recs = np.stack([D.pack(f.kp_cap, *f.fetch_image(2 * p), *f.fetch_image(2 * p + 1), f.fetch_stereo(p))
+                         for f in fes for p in range(P // S)])
         allrec = D.gather_results(recs, world * P, device=dev if dist.get_backend() == "nccl" else None)
         gather_s = time.perf_counter() - tg
         if rank == 0:
@@ -176,8 +194,10 @@ def main():
     if rank == 0:
         pairs_per_s = world * P * args.steps / elapsed
         total_b, per_stage_b = algorithmic_bytes_per_pair(args.width, args.height, args.nfeatures)
-        dom = max(stage_ms, key=stage_ms.get)
-        ach = per_stage_b[dom] * P / (stage_ms[dom] * 1e-3) / 1e9
+        # handle 0 holds P/S pairs as min(lanes, P/S) concurrent chunks; its stage events bracket chunk 0
+        chunk0 = (P // S) // max(1, min(args.lanes, P // S))
+        dom = max(stage_ms, key=stage_ms.get) if stage_ms else "detect"
+        ach = per_stage_b[dom] * chunk0 / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms else 0.0
         workload = f"kitti{args.width}x{args.height}_synth_{args.nfeatures}f_{P}pairs"
         tr = load_traffic(workload)
         out = {
@@ -195,7 +215,8 @@ def main():
             "data": "synthetic (seeded band-limited noise + rectangles, right = per-row-block disparity shift)",
             "config": {"workload": workload, "pairs_per_step_per_gpu": P, "width": args.width,
                        "height": args.height, "nfeatures": args.nfeatures, "nlevels": 8, "scaleFactor": 1.2,
-                       "iniThFAST": 20, "minThFAST": 7, "parallelism": f"pairs sharded {world}-way (replicas)"},
+                       "iniThFAST": 20, "minThFAST": 7, "parallelism": f"pairs sharded {world}-way (replicas)",
+                       "handles_per_gpu": S, "lanes_per_handle": args.lanes},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),

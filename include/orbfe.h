@@ -125,6 +125,11 @@ int orbfe_stereo_batch_device(orbfe_handle h, int32_t n_pairs, double bf, float 
 int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t img_pitch, int32_t n_pairs,
                                 double bf, float fx, void* hip_stream);
 
+/* orbfe_set_lanes: orbfe_frontend_batch_device runs its batch as min(lanes, n_pairs) contiguous chunks,
+ * each on an internal stream (fork from / join into the caller's stream); 1..4, default 4.  Results and
+ * their layout do not depend on it. */
+int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
+
 /* Device result layout of the last batch (pointers into handle-owned device memory):
  *   kps   : n_images x cap  orbfe_keypoint   (cap = *kp_cap)
  *   desc  : n_images x cap x 32 u8

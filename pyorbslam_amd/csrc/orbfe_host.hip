@@ -83,6 +83,9 @@ inline short sat_short(int v) { return (short)std::min(std::max(v, -32768), 3276
 
 }  // namespace
 
+// concurrent chunks of orbfe_frontend_batch_device (the box exposes 4 hardware queues per process)
+constexpr int kLanes = 4;
+
 struct orbfe_ctx {
     orbfe_params prm{};
     double scale_factor_d = 1.2;
@@ -134,8 +137,13 @@ struct orbfe_ctx {
     hipStream_t own_stream = nullptr;
     // k_blur runs on a side stream concurrently with k_detect / k_octree (fork after the pyramid, join
     // before k_describe); events only, so the batch stays capturable into a HIP graph
-    hipStream_t side_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side_stream[kLanes + 1] = {};
+    hipEvent_t ev_fork[kLanes + 1] = {}, ev_join[kLanes + 1] = {};
+    // orbfe_frontend_batch_device: up to kLanes concurrent chunks of the batch on internal streams
+    int lanes = kLanes;  // orbfe_set_lanes
+    hipStream_t lane_stream[kLanes] = {};
+    hipEvent_t lane_done[kLanes] = {};
+    hipEvent_t lane_fork = nullptr;
     hipStream_t last_stream = nullptr;
     const uint8_t* last_in = nullptr;  // device input of the last extraction
     int64_t last_pitch = 0;
@@ -147,9 +155,16 @@ struct orbfe_ctx {
     ~orbfe_ctx() {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
-        if (side_stream) (void)hipStreamDestroy(side_stream);
-        if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
+        for (int k = 0; k <= kLanes; ++k) {
+            if (side_stream[k]) (void)hipStreamDestroy(side_stream[k]);
+            if (ev_fork[k]) (void)hipEventDestroy(ev_fork[k]);
+            if (ev_join[k]) (void)hipEventDestroy(ev_join[k]);
+        }
+        for (int k = 0; k < kLanes; ++k) {
+            if (lane_stream[k]) (void)hipStreamDestroy(lane_stream[k]);
+            if (lane_done[k]) (void)hipEventDestroy(lane_done[k]);
+        }
+        if (lane_fork) (void)hipEventDestroy(lane_fork);
     }
 };
 
@@ -454,48 +469,74 @@ void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
     HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * (ORBFE_NSTAGES + 1) + k], s));
 }
 
-void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hipStream_t s) {
+// Images [i0, i0 + n) of the batch: every per-image buffer is passed at the chunk's offset, the
+// kernels index images from there.  prof: record stage boundaries on s.  fork_blur: run k_blur on the
+// side stream concurrently with k_detect / k_octree.
+void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int n, hipStream_t s, bool prof,
+                   bool fork_blur, int lane = -1) {
     const Geo& g = c.geo;
-    if (n <= 0) return;
+    const uint8_t* in = d_in + (int64_t)i0 * pitch;
+    uint8_t* ws = c.d_ws.p + (int64_t)i0 * g.ws_bytes;
+    uint8_t* blur = c.d_blur.p + (int64_t)i0 * g.blur_bytes;
+    int* cell_count = c.d_cell_count.p + (int64_t)i0 * g.ncells;
+    uint32_t* slots = c.d_slots.p + (int64_t)i0 * g.slot_total;
+    uint32_t* kd = c.d_kd.p + (int64_t)i0 * g.key_total;
+    uint16_t* kn = c.d_kn.p + (int64_t)i0 * g.key_total;
+    uint32_t* lvl_kp = c.d_lvl_kp.p + (int64_t)i0 * g.lvl_kp_cap;
+    int* lvl_count = c.d_lvl_count.p + (int64_t)i0 * g.nlevels;
+    orbfe_keypoint* kps = c.d_kps.p + (int64_t)i0 * g.kp_cap;
+    uint8_t* desc = c.d_desc.p + (int64_t)i0 * g.kp_cap * 32;
+    int* count = c.d_count.p + i0;
+    if (prof) prof_mark(c, s, 0);
+    for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
+    if (prof) prof_mark(c, s, 1);
+    if (fork_blur) {
+        // the blur of every level only needs the pyramid; it overlaps FAST and the octree, which are
+        // bound by VALU/LDS issue and latency rather than memory
+        const int k = lane + 1;  // side stream 0 serves the single-stream path, 1.. the lanes
+        if (!c.side_stream[k]) {
+            HIPCK(hipStreamCreateWithFlags(&c.side_stream[k], hipStreamNonBlocking));
+            HIPCK(hipEventCreateWithFlags(&c.ev_fork[k], hipEventDisableTiming));
+            HIPCK(hipEventCreateWithFlags(&c.ev_join[k], hipEventDisableTiming));
+        }
+        HIPCK(hipEventRecord(c.ev_fork[k], s));
+        HIPCK(hipStreamWaitEvent(c.side_stream[k], c.ev_fork[k], 0));
+        HIPCK(launch_blur(g, in, pitch, ws, blur, n, c.side_stream[k]));
+        HIPCK(hipEventRecord(c.ev_join[k], c.side_stream[k]));
+    }
+    if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
+    if (prof) prof_mark(c, s, 2);
+    HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
+                        s));
+    if (prof) prof_mark(c, s, 3);
+    if (fork_blur) HIPCK(hipStreamWaitEvent(s, c.ev_join[lane + 1], 0));  // join
+    else HIPCK(launch_blur(g, in, pitch, ws, blur, n, s));
+    HIPCK(launch_describe(g, in, pitch, ws, blur, lvl_kp, lvl_count, kps, desc, count, c.d_mw.p, n, s));
+    if (prof) prof_mark(c, s, 4);
+}
+
+void check_extract(orbfe_ctx& c, int64_t pitch, int n) {
+    const Geo& g = c.geo;
     if (n > c.max_images) throw Error(ORBFE_ECAPACITY, "batch larger than the reserved image count");
     if (pitch < (int64_t)g.W * g.H) throw Error(ORBFE_EINVAL, "image pitch smaller than width*height");
+}
+
+void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hipStream_t s) {
+    if (n <= 0) return;
+    check_extract(c, pitch, n);
     HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
-    prof_mark(c, s, 0);
-    for (int l = 1; l < g.nlevels; ++l)
-        HIPCK(launch_resize(g, l, d_in, pitch, c.d_ws.p, c.d_xt.p, c.d_yt.p, n, s));
-    prof_mark(c, s, 1);
-    // fork: the blur of every level only needs the pyramid; it overlaps FAST and the octree, which are
-    // bound by VALU/LDS issue and latency rather than memory
-    if (!c.side_stream) {
-        HIPCK(hipStreamCreateWithFlags(&c.side_stream, hipStreamNonBlocking));
-        HIPCK(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
-        HIPCK(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
-    }
-    HIPCK(hipEventRecord(c.ev_fork, s));
-    HIPCK(hipStreamWaitEvent(c.side_stream, c.ev_fork, 0));
-    HIPCK(launch_blur(g, d_in, pitch, c.d_ws.p, c.d_blur.p, n, c.side_stream));
-    HIPCK(hipEventRecord(c.ev_join, c.side_stream));
-    if (g.ncells > 0)
-        HIPCK(launch_detect(g, c.d_cells.p, d_in, pitch, c.d_ws.p, c.d_cell_count.p, c.d_slots.p, n, s));
-    prof_mark(c, s, 2);
-    HIPCK(launch_octree(g, c.d_cells.p, c.d_cell_count.p, c.d_slots.p, c.d_kd.p, c.d_kn.p, c.d_lvl_kp.p,
-                        c.d_lvl_count.p, c.d_overflow.p, c.maxcell, n, s));
-    prof_mark(c, s, 3);
-    HIPCK(hipStreamWaitEvent(s, c.ev_join, 0));  // join
-    HIPCK(launch_describe(g, d_in, pitch, c.d_ws.p, c.d_blur.p, c.d_lvl_kp.p, c.d_lvl_count.p, c.d_kps.p, c.d_desc.p,
-                          c.d_count.p, c.d_mw.p, n, s));
-    prof_mark(c, s, 4);
+    extract_range(c, d_in, pitch, 0, n, s, true, true);
     c.last_in = d_in;
     c.last_pitch = pitch;
     c.last_images = n;
     c.last_stream = s;
 }
 
-void stereo_buffers(orbfe_ctx& c, StereoArgs& a) {
-    a.bucket_off = c.d_boff.p;
-    a.bucket_idx = c.d_bidx.p;
+void stereo_buffers(orbfe_ctx& c, StereoArgs& a, int p0) {
+    a.bucket_off = c.d_boff.p + (int64_t)p0 * (c.geo.H + 1);
+    a.bucket_idx = c.d_bidx.p + (int64_t)p0 * c.bucket_cap;
     a.bucket_cap = c.bucket_cap;
-    a.rinfo = c.d_rinfo.p;
+    a.rinfo = c.d_rinfo.p + (int64_t)p0 * c.geo.kp_cap;
 }
 
 void stereo_consts(double bf, float fx, StereoArgs& a) {
@@ -506,38 +547,88 @@ void stereo_consts(double bf, float fx, StereoArgs& a) {
     a.bf = bf;
 }
 
-void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStream_t s) {
+// Pairs [p0, p0 + n) (images 2p, 2p + 1) of the extracted batch at d_in.
+void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int n, double bf, float fx,
+                  hipStream_t s) {
     const Geo& g = c.geo;
+    const int64_t i0 = 2 * (int64_t)p0;
+    StereoArgs a{};
+    a.kpsL = c.d_kps.p + i0 * g.kp_cap;
+    a.kpsR = a.kpsL + g.kp_cap;
+    a.kp_stride = 2 * (int64_t)g.kp_cap;
+    a.descL = c.d_desc.p + i0 * g.kp_cap * 32;
+    a.descR = a.descL + (int64_t)g.kp_cap * 32;
+    a.countL = c.d_count.p + i0;
+    a.countR = a.countL + 1;
+    a.cnt_stride = 2;
+    a.lvl0L = d_in + i0 * pitch;
+    a.lvl0R = a.lvl0L + pitch;
+    a.lvl0_stride = 2 * pitch;
+    a.wsL = c.d_ws.p + i0 * g.ws_bytes;
+    a.wsR = a.wsL + g.ws_bytes;
+    a.ws_stride = 2 * g.ws_bytes;
+    a.u_right = c.d_uR.p + (int64_t)p0 * g.kp_cap;
+    a.depth = c.d_depth.p + (int64_t)p0 * g.kp_cap;
+    a.status = c.d_status.p + (int64_t)p0 * g.kp_cap;
+    a.match_r = c.d_match.p + (int64_t)p0 * g.kp_cap;
+    a.out_stride = g.kp_cap;
+    stereo_buffers(c, a, p0);
+    stereo_consts(bf, fx, a);
+    HIPCK(launch_stereo(g, a, n, s));
+}
+
+void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStream_t s) {
     if (n_pairs <= 0) return;
     if (2 * n_pairs > c.last_images) throw Error(ORBFE_ESTATE, "stereo batch needs 2*n_pairs extracted images");
-    StereoArgs a{};
-    a.kpsL = c.d_kps.p;
-    a.kpsR = c.d_kps.p + g.kp_cap;
-    a.kp_stride = 2 * (int64_t)g.kp_cap;
-    a.descL = c.d_desc.p;
-    a.descR = c.d_desc.p + (int64_t)g.kp_cap * 32;
-    a.countL = c.d_count.p;
-    a.countR = c.d_count.p + 1;
-    a.cnt_stride = 2;
-    a.lvl0L = c.last_in;
-    a.lvl0R = c.last_in + c.last_pitch;
-    a.lvl0_stride = 2 * c.last_pitch;
-    a.wsL = c.d_ws.p;
-    a.wsR = c.d_ws.p + g.ws_bytes;
-    a.ws_stride = 2 * g.ws_bytes;
-    a.u_right = c.d_uR.p;
-    a.depth = c.d_depth.p;
-    a.status = c.d_status.p;
-    a.match_r = c.d_match.p;
-    a.out_stride = g.kp_cap;
-    stereo_buffers(c, a);
-    stereo_consts(bf, fx, a);
+    stereo_range(c, c.last_in, c.last_pitch, 0, n_pairs, bf, fx, s);
     c.last_bf = bf;
     c.last_fx = fx;
-    HIPCK(launch_stereo(g, a, n_pairs, s));
     prof_mark(c, s, 5);
     if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
     c.last_pairs = n_pairs;
+}
+
+// The whole front-end for n_pairs pairs as up to kLanes concurrent chunks, each on its own internal
+// stream (fork from / join into the caller's stream with events): the latency-bound stages of one chunk
+// overlap the issue-bound stages of another.  Chunk 0 carries the profiling marks.
+void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pairs, double bf, float fx,
+                      hipStream_t s) {
+    if (n_pairs <= 0) return;
+    check_extract(c, pitch, 2 * n_pairs);
+    HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
+    const int K = std::max(1, std::min(c.lanes, n_pairs));
+    if (K == 1) {
+        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true, true);
+        stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
+        prof_mark(c, s, 5);
+    } else {
+        if (!c.lane_stream[0]) {
+            for (int k = 0; k < kLanes; ++k) {
+                HIPCK(hipStreamCreateWithFlags(&c.lane_stream[k], hipStreamNonBlocking));
+                HIPCK(hipEventCreateWithFlags(&c.lane_done[k], hipEventDisableTiming));
+            }
+            HIPCK(hipEventCreateWithFlags(&c.lane_fork, hipEventDisableTiming));
+        }
+        HIPCK(hipEventRecord(c.lane_fork, s));
+        for (int k = 0; k < K; ++k) {
+            const int p0 = (int)((int64_t)n_pairs * k / K), p1 = (int)((int64_t)n_pairs * (k + 1) / K);
+            hipStream_t ls = c.lane_stream[k];
+            HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
+            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, true, k);
+            stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
+            if (k == 0) prof_mark(c, ls, 5);
+            HIPCK(hipEventRecord(c.lane_done[k], ls));
+        }
+        for (int k = 0; k < K; ++k) HIPCK(hipStreamWaitEvent(s, c.lane_done[k], 0));
+    }
+    if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
+    c.last_in = d_in;
+    c.last_pitch = pitch;
+    c.last_images = 2 * n_pairs;
+    c.last_pairs = n_pairs;
+    c.last_stream = s;
+    c.last_bf = bf;
+    c.last_fx = fx;
 }
 
 hipStream_t own(orbfe_ctx& c) {
@@ -681,7 +772,7 @@ int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, fl
         a.status = hl->d_status.p;
         a.match_r = hl->d_match.p;
         a.out_stride = g.kp_cap;
-        stereo_buffers(*hl, a);
+        stereo_buffers(*hl, a, 0);
         a.kp_stride = 0;
         stereo_consts(bf, fx, a);
         hipStream_t s = own(*hl);
@@ -721,8 +812,15 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
         if (!h || !d_images) throw Error(ORBFE_EINVAL, "null argument");
         if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
         h->have_single = false;
-        enqueue_extract(*h, d_images, img_pitch, 2 * n_pairs, (hipStream_t)hip_stream);
-        enqueue_stereo_batch(*h, n_pairs, bf, fx, (hipStream_t)hip_stream);
+        enqueue_frontend(*h, d_images, img_pitch, n_pairs, bf, fx, (hipStream_t)hip_stream);
+    });
+}
+
+int orbfe_set_lanes(orbfe_handle h, int32_t lanes) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (lanes < 1 || lanes > kLanes) throw Error(ORBFE_EINVAL, "lanes must be 1..4");
+        h->lanes = lanes;
     });
 }
 
