@@ -100,3 +100,23 @@ def test_batch_repeat_is_deterministic():
         r = fe.fetch_stereo(p)
         assert all(np.array_equal(first[p][k], r[k]) for k in r)
     assert fe.fetch_image(5)[0].tobytes() == k0[0].tobytes()
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+def test_lanes_do_not_change_results(lanes):
+    """orbfe_set_lanes splits the batch into concurrent chunks on internal streams (5 pairs: uneven
+    chunks); every image and pair must come out exactly as with one lane."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd.batch import StereoFrontEnd
+    imgs = torch.from_numpy(synth.make_batch(5, seed0=40)).cuda()
+    ref = StereoFrontEnd(max_pairs=5, lanes=1)
+    fe = StereoFrontEnd(max_pairs=5, lanes=lanes)
+    ref.enqueue(imgs)
+    fe.enqueue(imgs)
+    torch.cuda.synchronize()
+    for i in range(10):
+        a, b = ref.fetch_image(i), fe.fetch_image(i)
+        assert a[0].tobytes() == b[0].tobytes() and np.array_equal(a[1], b[1])
+    for p in range(5):
+        a, b = ref.fetch_stereo(p), fe.fetch_stereo(p)
+        assert all(np.array_equal(a[k], b[k]) for k in a)
