@@ -277,6 +277,24 @@ __device__ __forceinline__ fd_s2 fast_bound_pair(const uint32_t* R) {
     return __builtin_elementwise_max(v - fd_s(a), fd_s(b) - v);
 }
 
+// Upper bounds of the two adjacent pixel pairs at dwords R and R + 1 (pixels x .. x + 3), sharing the
+// cardinal rows: 6 dwords of the centre row, 2 above, 2 below.
+template <int S>
+__device__ __forceinline__ void fast_bound_quad(const uint32_t* R, fd_s2& bA, fd_s2& bB) {
+    const uint32_t m2 = R[-2], m1 = R[-1], z0 = R[0], p1 = R[1], p2 = R[2], p3 = R[3];
+    const uint32_t u0 = R[-3 * S], u1 = R[-3 * S + 1], d0 = R[3 * S], d1 = R[3 * S + 1];
+    auto bound = [](uint32_t v, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+        const fd_h2 h0 = fd_h(c0), h1 = fd_h(c1), h2 = fd_h(c2), h3 = fd_h(c3);
+        const fd_h2 a = fd_min(fd_min3(fd_max(h0, h1), fd_max(h1, h2), fd_max(h2, h3)), fd_max(h3, h0));
+        const fd_h2 b = fd_max(fd_max3(fd_min(h0, h1), fd_min(h1, h2), fd_min(h2, h3)), fd_min(h3, h0));
+        const fd_s2 vs = __builtin_bit_cast(fd_s2, v);
+        return __builtin_elementwise_max(vs - fd_s(a), fd_s(b) - vs);
+    };
+    // cardinals in circle order: 0 = (0, +3), 4 = (+3, 0), 8 = (0, -3), 12 = (-3, 0)
+    bA = bound(z0, d0, __builtin_amdgcn_alignbyte(p2, p1, 2), u0, __builtin_amdgcn_alignbyte(m1, m2, 2));
+    bB = bound(p1, d1, __builtin_amdgcn_alignbyte(p3, p2, 2), u1, __builtin_amdgcn_alignbyte(z0, m1, 2));
+}
+
 // Exact M of the pixel pair at dword R (row stride S dwords), as biased u16 x2.
 template <int S>
 __device__ __forceinline__ uint32_t fast_m_pair(const uint32_t* R) {
@@ -392,27 +410,33 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
                 return;
             }
         const int tq = min(g.ini_th, g.min_th);
-        // ---- 2. pre-test of every pair (row-major: lane -> pair i = i0 + lane)
-        const int prow = (ww + 1) >> 1, npair = prow * wh;
-        const int step_y = 64 / prow, step_x = 64 - step_y * prow;
+        // ---- 2. pre-test, two adjacent pairs (pixels x .. x + 3) per lane and step, quads in row-major
+        //         order (lane -> quad i0 + lane); the pair queue stays row-major (two ballots per step)
+        const int qrow = (ww + 3) >> 2, nquad = qrow * wh;
+        const int step_y = 64 / qrow, step_x = 64 - step_y * qrow;
         int npq = 0;
         {
-            int py = lane / prow, px = lane - (lane / prow) * prow;
-            for (int i0 = 0; i0 < npair; i0 += 64) {
-                bool cand = false;
-                if (i0 + lane < npair) {
-                    const int x = 2 * px;
-                    const fd_s2 pb = fast_bound_pair<S>((const uint32_t*)(roi + ((py & 63) + 3) * RP + x + 4));
-                    cand = pb.x > tq || (pb.y > tq && x + 1 < ww);
+            int qy = lane / qrow, qx = lane - (lane / qrow) * qrow;
+            for (int i0 = 0; i0 < nquad; i0 += 64) {
+                const int x = 4 * qx;
+                bool ca = false, cb = false;
+                if (i0 + lane < nquad) {
+                    fd_s2 ba, bb;
+                    fast_bound_quad<S>((const uint32_t*)(roi + ((qy & 63) + 3) * RP + x + 4), ba, bb);
+                    ca = ba.x > tq || (ba.y > tq && x + 1 < ww);
+                    cb = x + 2 < ww && (bb.x > tq || (bb.y > tq && x + 3 < ww));
                 }
-                const uint64_t bal = __ballot(cand);
-                if (cand) pq[npq + lanes_below(bal)] = (uint16_t)((py << 6) | (2 * px));
-                npq += __popcll(bal);
-                py += step_y;
-                px += step_x;
-                if (px >= prow) {
-                    px -= prow;
-                    ++py;
+                const uint64_t b0 = __ballot(ca), b1 = __ballot(cb);
+                const int o = npq + lanes_below(b0) + lanes_below(b1);
+                const uint16_t e = (uint16_t)((qy << 6) | x);
+                if (ca) pq[o] = e;
+                if (cb) pq[o + (int)ca] = (uint16_t)(e + 2);
+                npq += __popcll(b0) + __popcll(b1);
+                qy += step_y;
+                qx += step_x;
+                if (qx >= qrow) {
+                    qx -= qrow;
+                    ++qy;
                 }
             }
         }
