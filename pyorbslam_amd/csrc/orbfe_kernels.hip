@@ -27,6 +27,8 @@ __constant__ __attribute__((aligned(16))) float c_pattern[1024] = {
 };
 
 // ------------------------------------------------------------------------------- small helpers
+typedef float df2 __attribute__((ext_vector_type(2)));  // packed f32 (v_pk_mul/fma/add_f32)
+
 // Buffer resource for a wave-uniform base pointer: loads take a 32-bit lane offset (no 64-bit address
 // arithmetic per lane).  Dword 3 = 0x00020000, the gfx9 raw-buffer format word.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
@@ -1305,8 +1307,11 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
-            const uint32_t fr = __float_as_uint(__fadd_rn(fmaf(px, b, __fmul_rn(py, a)), 12582912.0f));
-            const uint32_t fc = __float_as_uint(__fadd_rn(fmaf(px, a, -__fmul_rn(py, b)), 12582912.0f));
+            // (row, col) = (fma(px, b, py a), fma(px, a, -(py b))) as packed f32: v_pk_mul + v_pk_fma + v_pk_add,
+            // each half rounded exactly like the scalar expression
+            const df2 m = (df2){py, py} * (df2){a, -b};
+            const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, m) + (df2){12582912.0f, 12582912.0f};
+            const uint32_t fr = __float_as_uint(rc.x), fc = __float_as_uint(rc.y);
             val[2 * i + e] = __builtin_amdgcn_raw_buffer_load_b8(br, (fr & 0xFFFFFFu) * pitch24 + fc + boff, 0, 0);
         }
     }
