@@ -1067,8 +1067,35 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    {
-        constexpr int NS = (kBlurWR * kBlurWD + 255) / 256;
+    constexpr int NS = (kBlurWR * kBlurWD + 255) / 256;
+    // interior tiles (no reflected rows or columns, every dword inside the level): buffer loads at 32-bit
+    // offsets, slot -> (row, dword) by a 24-bit multiply (slot / 18 == (slot * 3641) >> 16 for slot < 1152)
+    const bool interior = Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h && X0 >= 4 && X0 - 4 + 4 * kBlurWD + 4 <= L.w;
+    if (interior) {
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(lvl);
+        const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
+        const uint32_t base = (uint32_t)((Y0 - 3) * stride + X0 - 4);
+        uint2 raw[NS];
+        uint32_t sh[NS];
+        int dst[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const uint32_t slot = (uint32_t)(t + 256 * k);
+            const uint32_t r = __umul24(slot, 3641u) >> 16, d = slot - 18u * r;
+            raw[k] = uint2{0u, 0u};
+            sh[k] = 0;
+            dst[k] = -1;
+            if (slot < (uint32_t)(kBlurWR * kBlurWD)) {
+                const uint32_t off = base + __umul24(r, (uint32_t)stride & 0xFFFFFFu) + 4u * d;
+                sh[k] = (lvl_lo + off) & 3u;
+                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off - sh[k], 0, 0));
+                dst[k] = (int)(r * kBlurSD + d);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (dst[k] >= 0) src[dst[k]] = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh[k]);
+    } else {
         uint32_t lo[NS], hi[NS];
         int sh[NS], dst[NS];
 #pragma unroll
