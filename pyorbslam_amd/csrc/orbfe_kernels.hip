@@ -1068,13 +1068,18 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
     constexpr int NS = (kBlurWR * kBlurWD + 255) / 256;
-    // interior tiles (no reflected rows or columns, every dword inside the level): buffer loads at 32-bit
-    // offsets, slot -> (row, dword) by a 24-bit multiply (slot / 18 == (slot * 3641) >> 16 for slot < 1152)
-    const bool interior = Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h && X0 >= 4 && X0 - 4 + 4 * kBlurWD + 4 <= L.w;
-    if (interior) {
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(lvl);
-        const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
-        const uint32_t base = (uint32_t)((Y0 - 3) * stride + X0 - 4);
+    // staging: buffer dwordx2 loads at 32-bit offsets, the resource bounded by the level's extent (reads
+    // past it return 0, never fault); slot -> (row, dword) by a 24-bit multiply (slot / 18 ==
+    // (slot * 3641) >> 16 for slot < 1152); rows through reflect-101 only on tiles that reach past the
+    // top or bottom; dwords left of column 0 or right of w-1 are skipped (patched from LDS below)
+    {
+        const bool yb = !(Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h);
+        const uint64_t a64 = (uint64_t)(uintptr_t)lvl;
+        const uint32_t alo = __builtin_amdgcn_readfirstlane((uint32_t)a64);
+        const uint32_t ahi = __builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(((uint64_t)ahi << 32) | alo), 0, stride * L.h, 0x00020000);
+        const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;
         uint2 raw[NS];
         uint32_t sh[NS];
         int dst[NS];
@@ -1082,12 +1087,15 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
         for (int k = 0; k < NS; ++k) {
             const uint32_t slot = (uint32_t)(t + 256 * k);
             const uint32_t r = __umul24(slot, 3641u) >> 16, d = slot - 18u * r;
+            const int x = X0 - 4 + 4 * (int)d;  // image column of the dword's first byte
             raw[k] = uint2{0u, 0u};
             sh[k] = 0;
             dst[k] = -1;
-            if (slot < (uint32_t)(kBlurWR * kBlurWD)) {
-                const uint32_t off = base + __umul24(r, (uint32_t)stride & 0xFFFFFFu) + 4u * d;
-                sh[k] = (lvl_lo + off) & 3u;
+            if (slot < (uint32_t)(kBlurWR * kBlurWD) && x >= 0 && x < L.w) {
+                int ry = Y0 - 3 + (int)r;
+                if (yb) ry = reflect101c(ry, L.h);
+                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)x;
+                sh[k] = (alo + off) & 3u;
                 raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off - sh[k], 0, 0));
                 dst[k] = (int)(r * kBlurSD + d);
             }
@@ -1095,30 +1103,6 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < NS; ++k)
             if (dst[k] >= 0) src[dst[k]] = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh[k]);
-    } else {
-        uint32_t lo[NS], hi[NS];
-        int sh[NS], dst[NS];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const int slot = t + 256 * k;
-            const int r = slot / kBlurWD, d = slot - r * kBlurWD;
-            const int x = X0 - 4 + 4 * d;  // image column of the dword's first byte
-            dst[k] = -1;
-            lo[k] = hi[k] = 0;
-            sh[k] = 0;
-            if (r < kBlurWR && x >= 0 && x < L.w) {
-                const uint8_t* row = lvl + (int64_t)reflect101c(Y0 - 3 + r, L.h) * stride;
-                const uintptr_t a = (uintptr_t)(row + x);
-                const uint32_t* p = (const uint32_t*)(a & ~(uintptr_t)3);
-                sh[k] = (int)(a & 3);
-                lo[k] = p[0];
-                if (sh[k] != 0 && (const uint8_t*)(p + 1) < row + L.w) hi[k] = p[1];
-                dst[k] = r * kBlurSD + d;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            if (dst[k] >= 0) src[dst[k]] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
     }
     const bool left = X0 == 0, right = X0 + kBlurTX + 4 > L.w;
     if (left || right) {  // patch the reflected columns (sources lie inside the window, never patched)
