@@ -4,8 +4,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -Wall \
             -munsafe-fp-atomics -Wno-unused-result
-SRC := pyorbslam_amd/csrc/orbfe_kernels.hip pyorbslam_amd/csrc/orbfe_host.hip
-HDR := pyorbslam_amd/csrc/orbfe_common.h pyorbslam_amd/csrc/orbfe_kernels.h include/orbfe.h \
+SRC := pyorbslam_amd/csrc/orbfe_kernels.hip pyorbslam_amd/csrc/orbfe_host.hip pyorbslam_amd/csrc/orbfe_vocab.hip
+HDR := pyorbslam_amd/csrc/orbfe_common.h pyorbslam_amd/csrc/orbfe_kernels.h pyorbslam_amd/csrc/orbfe_host_util.h include/orbfe.h \
        pyorbslam_amd/csrc/brief_pattern.inc
 LIB := pyorbslam_amd/_lib/liborbfe.so
 OBJ := $(patsubst pyorbslam_amd/csrc/%.hip,pyorbslam_amd/_lib/%.o,$(SRC))

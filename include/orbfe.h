@@ -8,6 +8,8 @@
  *   Frame.compute_stereo_matches           Frame.py:161-279
  *   ORBMatcher.descriptor_distance / search_by_projection_f_f / _f_p (Hamming core)
  *                                          ORBMatcher.py:12-14, 215-283, 291-393
+ *   pyDBoW.TemplatedVocabulary load_from_text_file / transform / transform_feature
+ *                                          pyDBoW/TemplatedVocabulary.py:43-81, 108-160
  *
  * Conventions
  *   - plain C types only; caller-owned output buffers; every call returns an int status
@@ -34,6 +36,8 @@ extern "C" {
 #define ORBFE_ECAPACITY (-4) /* caller buffer too small (*n_out holds the need)     */
 #define ORBFE_ESTATE (-5)    /* call order violated (e.g. pyramid before extract)   */
 #define ORBFE_EOVERFLOW (-6) /* an on-device capacity bound was exceeded            */
+#define ORBFE_EFORMAT (-7)   /* malformed input file (vocabulary text)              */
+#define ORBFE_EREJECT (-8)   /* vocabulary header outside the accepted ranges       */
 
 /* ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
  * (orb_extractor.cpp:23; ORBextractor.cpp:410-470). */
@@ -207,6 +211,53 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
 /* orbfe_debug_octree_profile: re-runs the last batch's octree stage with wall-clock marks (100 MHz ticks,
  * 64 per (image, level), 0 = not reached) written by each workgroup's first thread; development aid. */
 int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n);
+
+/* ---- bag-of-words vocabulary (pyDBoW/TemplatedVocabulary.py) ---------------------------
+ *
+ * A vocabulary tree of ORB descriptors.  Node 0 is the root; every other node has a parent with a
+ * smaller id, and a node's children are ordered by id (the order TemplatedVocabulary.py:62-79 appends
+ * them).  A node is a leaf when it has no children (Node.is_leaf, TemplatedVocabulary.py:19-20);
+ * word ids number the nodes FLAGGED as leaves in id order (other nodes report word 0).  Parsing and
+ * the node tables live on the host; the device copy is made on the first transform. */
+typedef struct orbfe_vocab* orbfe_vocab_handle;
+
+typedef struct orbfe_vocab_info {
+    int32_t k, L;              /* header branching factor and depth (TemplatedVocabulary.py:46-47) */
+    int32_t scoring, weighting; /* header codes n1, n2 (TemplatedVocabulary.py:48-49, 55-56)     */
+    int64_t n_nodes;           /* including the root                                            */
+    int64_t n_words;           /* flagged leaves: TemplatedVocabulary.size()                    */
+    int32_t depth;             /* longest root-to-leaf path                                     */
+    int32_t max_children;
+} orbfe_vocab_info;
+
+/* TemplatedVocabulary.load_from_text_file (TemplatedVocabulary.py:43-81), parsed natively.
+ * Header "k L n1 n2"; ORBFE_EREJECT when 0<=k<=20, 1<=L<=10, 0<=n1<=5, 0<=n2<=3 fails (the
+ * reference prints a message and returns False).  Each following line: parent is_leaf d0..d31
+ * weight, with byte values in [0,255] and parent < node id; anything else is ORBFE_EFORMAT. */
+int orbfe_vocab_load_text(const char* path, orbfe_vocab_handle* out);
+/* The same tree from arrays: n_nodes entries each (entry 0 = root, its parent/desc ignored). */
+int orbfe_vocab_create(int32_t k, int32_t L, int32_t scoring, int32_t weighting, int64_t n_nodes,
+                       const int32_t* parent, const uint8_t* is_leaf, const uint8_t* desc32, const double* weight,
+                       orbfe_vocab_handle* out);
+int orbfe_vocab_destroy(orbfe_vocab_handle v);
+int orbfe_vocab_get_info(orbfe_vocab_handle v, orbfe_vocab_info* info);
+/* Host copies of the node tables (any pointer may be NULL); n_nodes entries each. */
+int orbfe_vocab_get_nodes(orbfe_vocab_handle v, int32_t* parent, uint8_t* is_leaf, uint8_t* desc32, double* weight,
+                          int32_t* word_id);
+
+/* Descent of n descriptors (TemplatedVocabulary.transform_feature, TemplatedVocabulary.py:131-160):
+ * from the root, move to the child at the smallest Hamming distance (first child on ties) until a
+ * node without children.  word_id / weight are that node's; node_id is the node entered at depth
+ * nid_level, or -1 when the descent stopped above it (the reference then keeps the previous
+ * feature's value, which the caller threads; TemplatedVocabulary.py:118-123).  Host buffers,
+ * synchronous. */
+int orbfe_vocab_transform(orbfe_vocab_handle v, const uint8_t* desc32, int64_t n, int32_t nid_level,
+                          int32_t* word_id, int32_t* node_id, double* weight);
+/* Same on device pointers, enqueued on hip_stream (void* = hipStream_t) without synchronising. */
+int orbfe_vocab_transform_device(orbfe_vocab_handle v, const uint8_t* d_desc32, int64_t n, int32_t nid_level,
+                                 int32_t* d_word_id, int32_t* d_node_id, double* d_weight, void* hip_stream);
+/* Kernel time of the last orbfe_vocab_transform (ms, HIP events), for measurement. */
+int orbfe_vocab_last_ms(orbfe_vocab_handle v, float* ms);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,10 @@ import numpy as np
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "liborbfe.so"
 
 ORBFE_OK = 0
-ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ESTATE", -6: "EOVERFLOW"}
+ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ESTATE", -6: "EOVERFLOW", -7: "EFORMAT",
+          -8: "EREJECT"}
+ORBFE_EFORMAT = -7
+ORBFE_EREJECT = -8
 
 
 class Params(C.Structure):
@@ -26,6 +29,11 @@ class BatchView(C.Structure):
     _fields_ = [("kp_cap", C.c_int32), ("n_images", C.c_int32), ("n_pairs", C.c_int32),
                 ("kps", C.c_void_p), ("desc", C.c_void_p), ("count", C.c_void_p), ("u_right", C.c_void_p),
                 ("depth", C.c_void_p), ("status", C.c_void_p), ("match_r", C.c_void_p), ("overflow", C.c_void_p)]
+
+
+class VocabInfo(C.Structure):
+    _fields_ = [("k", C.c_int32), ("L", C.c_int32), ("scoring", C.c_int32), ("weighting", C.c_int32),
+                ("n_nodes", C.c_int64), ("n_words", C.c_int64), ("depth", C.c_int32), ("max_children", C.c_int32)]
 
 
 # cv::KeyPoint tuple layout (opencv_type_casters.h:106-108)
@@ -64,6 +72,16 @@ SIGNATURES = {
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
     "orbfe_set_lanes": [C.c_void_p, C.c_int32],
+    "orbfe_vocab_load_text": [C.c_char_p, C.POINTER(C.c_void_p)],
+    "orbfe_vocab_create": [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                           C.c_void_p, C.POINTER(C.c_void_p)],
+    "orbfe_vocab_destroy": [C.c_void_p],
+    "orbfe_vocab_get_info": [C.c_void_p, C.POINTER(VocabInfo)],
+    "orbfe_vocab_get_nodes": [C.c_void_p] * 6,
+    "orbfe_vocab_transform": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p],
+    "orbfe_vocab_transform_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p],
+    "orbfe_vocab_last_ms": [C.c_void_p, C.POINTER(C.c_float)],
 }
 
 _lib: C.CDLL | None = None
