@@ -298,6 +298,9 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     g.fd_mp = std::max(g.fd_mp, (ww + 6 + 7) & ~7);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
+                    // k_detect stages the minTh survivors (u32) in the pixel queue (max_win u16)
+                    if (4 * cg.slot_cap > 2 * ((ww * wh + 15) & ~15))
+                        throw Error(ORBFE_EINVAL, "FAST cell too small for the NMS staging area");
                     slot_off += cg.slot_cap;
                     key_cap += cg.slot_cap;
                     c.cells.push_back(cg);

@@ -246,14 +246,16 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 //     circularly adjacent cardinal pairs (circle points 0, 4, 8, 12) bounds M from above, because every
 //     arc of 9 contains such a pair.  Pairs with P <= tq = min(iniTh, minTh) in both pixels have M <= tq:
 //     neither corners nor relevant NMS neighbours at either threshold; they keep M = 0.  The others are
-//     queued in row-major order (ballot + mbcnt).
+//     queued in row-major order (ballot + mbcnt).  (Queueing single pixels halves the M work per pixel
+//     but not per cell: a cell's queue is a few 64-entry steps either way, measured slower.)
 //  3. Exact M of the queued pairs -> a biased u16 M map with a zero (0x3C00) border; pixels with
 //     M > max(tq, 1) are queued (row-major: two ballots per step) for NMS.
 //  4. NMS over that queue.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the
 //     window or not corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour
-//     with M <= t is below M anyway.  So the local-max test is threshold independent and the
-//     iniTh -> minTh fallback (ORBextractor.cpp:811-815) only changes the cut M > max(t, 1).  Kept
-//     pixels are written in the queue's row-major order, i.e. cv::FAST's output order.
+//     with M <= t is below M anyway.  So the local-max test is threshold independent: one pass decides
+//     iniTh and minTh together, and the iniTh -> minTh fallback (ORBextractor.cpp:811-815) only picks
+//     which survivor list is kept.  Kept pixels are written in the queue's row-major order, i.e.
+//     cv::FAST's output order.
 typedef _Float16 fd_h2 __attribute__((ext_vector_type(2)));
 typedef short fd_s2 __attribute__((ext_vector_type(2)));
 
@@ -473,31 +475,46 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
             if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
             return;
         }
-        // ---- 4. NMS (local max) over the queue + ordered compaction at iniTh, else minTh
+        // ---- 4. NMS (local max) over the queue + ordered compaction, both thresholds in one pass: the
+        //         neighbour maximum does not depend on t, so each entry is tested at iniTh and minTh
+        //         together.  iniTh survivors go straight out; minTh survivors are staged in the (free) pixel
+        //         queue area and copied out only if iniTh kept nothing (ORBextractor.cpp:811-815).
         uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-        int total = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            const int thb = 0x3C00 + max(pass == 0 ? g.ini_th : g.min_th, 1);
-            total = 0;
-            for (int k0 = 0; k0 < nnq; k0 += 64) {
-                bool keep = false;
-                int e = 0, own = 0;
-                if (k0 + lane < nnq) {
-                    e = nq[k0 + lane];
-                    const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
-                    own = q[0];
-                    const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]), imax3(q[MP - 1], q[MP], q[MP + 1]));
-                    keep = own > max(imax3(nmax, q[-1], q[1]), thb);
-                }
-                const uint64_t bal = __ballot(keep);
-                const int o = total + lanes_below(bal);
-                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-                if (keep && o < cg.slot_cap)
-                    out[o] = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
-                             ((uint32_t)((own & 0xFF) - 1) << 24);
-                total += __popcll(bal);
+        uint32_t* alt = (uint32_t*)pq;  // 4 * slot_cap <= 2 * max_win bytes (checked on the host)
+        const bool fb = g.min_th != g.ini_th;
+        const int thb0 = 0x3C00 + max(g.ini_th, 1), thb1 = 0x3C00 + max(g.min_th, 1);
+        int t0 = 0, t1 = 0;
+        for (int k0 = 0; k0 < nnq; k0 += 64) {
+            bool keep0 = false, keep1 = false;
+            uint32_t rec = 0;
+            if (k0 + lane < nnq) {
+                const int e = nq[k0 + lane];
+                const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
+                const int own = q[0];
+                const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]),
+                                     imax3(q[MP - 1], q[MP], max(q[MP + 1], max(q[-1], q[1]))));
+                keep0 = own > max(nmax, thb0);
+                keep1 = own > max(nmax, thb1);
+                rec = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
+                      ((uint32_t)((own & 0xFF) - 1) << 24);
             }
-            if (total > 0 || g.min_th == g.ini_th) break;
+            const uint64_t bal0 = __ballot(keep0);
+            const int o0 = t0 + lanes_below(bal0);
+            // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+            if (keep0 && o0 < cg.slot_cap) out[o0] = rec;
+            t0 += __popcll(bal0);
+            if (fb) {
+                const uint64_t bal1 = __ballot(keep1);
+                const int o1 = t1 + lanes_below(bal1);
+                if (keep1 && o1 < cg.slot_cap) alt[o1] = rec;
+                t1 += __popcll(bal1);
+            }
+        }
+        int total = t0;
+        if (t0 == 0 && t1 > 0) {
+            __syncthreads();
+            for (int i = lane; i < min(t1, cg.slot_cap); i += 64) out[i] = alt[i];
+            total = t1;
         }
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
         };
