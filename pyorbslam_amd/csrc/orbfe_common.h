@@ -87,7 +87,8 @@ struct Geo {
     int max_rw;          // largest FAST cell ROI width (columns)
     int max_wh;          // largest FAST detection window height (rows)
     int max_win;         // largest FAST detection window (pixels), rounded up to 16
-    int fd_mp;           // k_detect: M map pitch in u16 (>= widest window + 6, multiple of 8)
+    int fd_mp;           // k_detect: u8 M map pitch in bytes (>= widest window + 6, multiple of 16)
+    int fd_pq;           // k_detect: pair-queue entries (>= ceil(ww/2) * wh and >= 2 * slot_cap)
     int umax[16];
     float scale[kMaxLevels];
     float inv_scale[kMaxLevels];

@@ -295,12 +295,11 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     g.max_rw = std::max(g.max_rw, rw);
                     g.max_wh = std::max(g.max_wh, wh);
                     g.max_win = std::max(g.max_win, (ww * wh + 15) & ~15);
-                    g.fd_mp = std::max(g.fd_mp, (ww + 6 + 7) & ~7);
+                    g.fd_mp = std::max(g.fd_mp, (ww + 6 + 15) & ~15);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
-                    // k_detect stages the minTh survivors (u32) in the pixel queue (max_win u16)
-                    if (4 * cg.slot_cap > 2 * ((ww * wh + 15) & ~15))
-                        throw Error(ORBFE_EINVAL, "FAST cell too small for the NMS staging area");
+                    // k_detect's pair queue also stages the minTh survivors (u32 = 2 entries each)
+                    g.fd_pq = std::max(g.fd_pq, (std::max(((ww + 1) / 2) * wh, 2 * cg.slot_cap) + 7) & ~7);
                     slot_off += cg.slot_cap;
                     key_cap += cg.slot_cap;
                     c.cells.push_back(cg);

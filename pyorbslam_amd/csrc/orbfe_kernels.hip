@@ -248,8 +248,9 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 //     neither corners nor relevant NMS neighbours at either threshold; they keep M = 0.  The others are
 //     queued in row-major order (ballot + mbcnt).  (Queueing single pixels halves the M work per pixel
 //     but not per cell: a cell's queue is a few 64-entry steps either way, measured slower.)
-//  3. Exact M of the queued pairs -> a biased u16 M map with a zero (0x3C00) border; pixels with
-//     M > max(tq, 1) are queued (row-major: two ballots per step) for NMS.
+//  3. Exact M of the queued pairs -> a u8 M map with a zero border (half the LDS of a u16 map: detect is
+//     occupancy-bound, one 64-thread workgroup per wave); pixels with M > max(tq, 1) are queued
+//     (row-major: two ballots per step) for NMS.
 //  4. NMS over that queue.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the
 //     window or not corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour
 //     with M <= t is below M anyway.  So the local-max test is threshold independent: one pass decides
@@ -345,9 +346,9 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* roi = (uint16_t*)lds;                            // max_rh rows x RP
     const int MP = g.fd_mp & 0xFFFF;  // provably 16-bit: row offsets use v_mul_u32_u24
-    uint16_t* mm = roi + RP * g.max_rh;                        // (max_wh + 2) x MP: window px (x, y) at (y + 1) * MP + x + 2
-    uint16_t* pq = mm + MP * (g.max_wh + 2);                   // pair queue: (y << 6) | x
-    uint16_t* nq = pq + g.max_win;                             // NMS queue: (y << 6) | x
+    uint8_t* mm = (uint8_t*)(roi + RP * g.max_rh);             // u8 M, (max_wh + 2) x MP: px (x, y) at (y + 1) * MP + x + 2
+    uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));      // pair queue: (y << 6) | x  (fd_pq entries)
+    uint16_t* nq = pq + g.fd_pq;                               // NMS queue: (y << 6) | x  (max_win entries)
     const int img = blockIdx.y, lane = threadIdx.x;
     const int c_first = blockIdx.x * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
     // ROI staging, 16 lanes per row (dword d), 4 rows per step (up to 16 steps = 64 rows): each slot is
@@ -399,8 +400,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
             }
             // the M map with its zero border
             uint4* m128 = (uint4*)mm;
-            const uint4 z = uint4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};
-            for (int i = lane; i < (MP / 8) * (wh + 2); i += 64) m128[i] = z;
+            for (int i = lane; i < (MP / 16) * (wh + 2); i += 64) m128[i] = uint4{0u, 0u, 0u, 0u};
         }
         if (c + 1 < c_last) issue(c + 1);  // in flight during this cell's compute
         __syncthreads();
@@ -460,7 +460,8 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
                 const int x = e & 63, y = e >> 6;
                 uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
                 if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
-                *(uint32_t*)(mm + (y + 1) * MP + x + 2) = m;
+                // the u8 map keeps M itself (low byte of each biased half)
+                *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
                 h0 = (int)(m & 0x3FFu) > tlow;
                 h1 = (int)((m >> 16) & 0x3FFu) > tlow;
             }
@@ -480,23 +481,23 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
         //         together.  iniTh survivors go straight out; minTh survivors are staged in the (free) pixel
         //         queue area and copied out only if iniTh kept nothing (ORBextractor.cpp:811-815).
         uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-        uint32_t* alt = (uint32_t*)pq;  // 4 * slot_cap <= 2 * max_win bytes (checked on the host)
+        uint32_t* alt = (uint32_t*)pq;  // 2 * slot_cap <= fd_pq entries (host)
         const bool fb = g.min_th != g.ini_th;
-        const int thb0 = 0x3C00 + max(g.ini_th, 1), thb1 = 0x3C00 + max(g.min_th, 1);
+        const int thb0 = max(g.ini_th, 1), thb1 = max(g.min_th, 1);
         int t0 = 0, t1 = 0;
         for (int k0 = 0; k0 < nnq; k0 += 64) {
             bool keep0 = false, keep1 = false;
             uint32_t rec = 0;
             if (k0 + lane < nnq) {
                 const int e = nq[k0 + lane];
-                const uint16_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
+                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
                 const int own = q[0];
                 const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]),
                                      imax3(q[MP - 1], q[MP], max(q[MP + 1], max(q[-1], q[1]))));
                 keep0 = own > max(nmax, thb0);
                 keep1 = own > max(nmax, thb1);
                 rec = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
-                      ((uint32_t)((own & 0xFF) - 1) << 24);
+                      ((uint32_t)(own - 1) << 24);
             }
             const uint64_t bal0 = __ballot(keep0);
             const int o0 = t0 + lanes_below(bal0);
@@ -1647,13 +1648,16 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 int detect_rp(const Geo& g) { return g.max_rw + 3 <= 48 ? 48 : g.max_rw + 3 <= 64 ? 64 : 96; }
 
 size_t detect_lds_bytes(const Geo& g) {
-    return 2 * ((size_t)detect_rp(g) * g.max_rh + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.max_win);
+    return 2 * (size_t)detect_rp(g) * g.max_rh + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.fd_pq +
+           2 * (size_t)g.max_win;
 }
 
 template <int RP>
 static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                              int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
-    const size_t lds = detect_lds_bytes(g);
+    // variants 8 / 9: the full kernel with 6 / 12 KiB of extra (unused) LDS, to measure how detect
+    // time depends on occupancy (tools/microbench.py)
+    const size_t lds = detect_lds_bytes(g) + (variant == 8 ? 6144 : variant == 9 ? 12288 : 0);
     const dim3 grid((g.ncells + kFdCells - 1) / kFdCells, n_images), blk(64);
     auto k = variant == 1 ? k_detect<1, RP> : variant == 2 ? k_detect<2, RP> : variant == 3 ? k_detect<3, RP>
                                                                                            : k_detect<0, RP>;
