@@ -11,7 +11,8 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "_lib" / "liborbfe.so"
+# ORBFE_LIB selects another in-tree build of the same C-ABI (same-box A/B of kernel revisions)
+LIB_PATH = Path(os.environ.get("ORBFE_LIB") or Path(__file__).resolve().parent / "_lib" / "liborbfe.so")
 
 ORBFE_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ESTATE", -6: "EOVERFLOW", -7: "EFORMAT",
@@ -102,7 +103,11 @@ def lib() -> C.CDLL:
                           "pyorbslam_amd has no CPU fallback")
         L = C.CDLL(str(LIB_PATH))
         for name, argtypes in SIGNATURES.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None and os.environ.get("ORBFE_LIB"):
+                continue  # an older revision under A/B may predate some entry points
+            if fn is None:
+                raise OSError(f"{LIB_PATH} does not export {name}")
             fn.argtypes = argtypes
             fn.restype = C.c_char_p if name in ("orbfe_last_error", "orbfe_version") else C.c_int
         _lib = L

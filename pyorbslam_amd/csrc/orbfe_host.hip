@@ -963,6 +963,7 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
+                    // variant 0 blur + describe, 1 blur, 2 describe
                     if (variant != 2)
                         HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s));
                     if (variant != 1)

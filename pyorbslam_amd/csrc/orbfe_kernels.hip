@@ -1212,6 +1212,8 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
 //  each row's descriptor, kept by sub-lane i and stored as one u16 per lane.
 // Blocks are remapped XCD-aware: each XCD's L2 receives a contiguous run of waves (consecutive
 // keypoints are spatial neighbours in octree order and share cache lines).
+constexpr int kDescWinRows = 37;  // sample rows cy - 18 .. cy + 18
+
 __device__ __forceinline__ int row16_sum(int v) {  // sum over the lane's 16-lane DPP row
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
@@ -1229,6 +1231,9 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     __shared__ float4 s_pat[256];
     // per (row shift sh, window slot): the byte mask of the umax disc and the dot4 weights of m10
     __shared__ uint2 s_mw[4][31 * 9];
+    // per wave and keypoint row: the blurred 37 x 37 sample window (rows cy - 18 .. cy + 18), staged with
+    // dwordx4 loads from the dword-aligned column at or left of cx - 18; 48 bytes per window row
+    __shared__ uint4 s_win[kDescWaves][4][kDescWinRows * 3];
     // XCD-aware remap of the flattened grid: hardware block i runs on XCD i % 8
     const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
     const int per = nb >> 3;
@@ -1292,6 +1297,27 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
             }
         }
     }
+    // ---- blurred sample window: 37 rows x 3 dwordx4 = 111 slots, sub-lane sl takes slots sl + 16 k
+    //      (16 = 5 rows + 1 column), loads in flight during the centroid arithmetic
+    const __amdgpu_buffer_rsrc_t br = uniform_rsrc(blur + (int64_t)img * g.blur_bytes + L.blur_off);
+    const uint32_t win0 = (uint32_t)((cy - 18) * L.pitch + ((cx - 18) & ~3));
+    uint4 wv4[7];
+    {
+        int r = sl / 3, c = sl - 3 * (sl / 3);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            wv4[k] = uint4{0u, 0u, 0u, 0u};
+            if (r < kDescWinRows)
+                wv4[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       br, win0 + (uint32_t)r * (uint32_t)L.pitch + 16u * c, 0, 0));
+            r += 5;
+            c += 1;
+            if (c >= 3) {
+                c -= 3;
+                r += 1;
+            }
+        }
+    }
     // m10 = sum (u0 + b) val_b, m01 = sum v val_b with non-negative byte weights (u0 + 18 + b), (v + 15)
     // accumulated by v_dot4 and corrected by -18 / -15 x sum(val); masks and m10 weights from s_mw
     uint32_t a10 = 0, a01 = 0, a1 = 0;
@@ -1321,14 +1347,29 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
     const float angle = fast_atan2((float)m01, (float)m10);
     float b, a;
     glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
-    // ---- steered BRIEF: 32 samples per lane (|offset| <= 13 * sqrt 2 < 19), 32-bit offsets from the
-    // corner (cy - 19, cx - 19), which is >= 0: detection windows start 19 pixels inside every level
-    const __amdgpu_buffer_rsrc_t br = uniform_rsrc(blur + (int64_t)img * g.blur_bytes + L.blur_off);
+    // ---- steered BRIEF: 32 samples per lane (|offset| <= 13 * sqrt 2 < 18.4, so |rint| <= 18) read from
+    //      the staged window in LDS: window byte (18 + row) * 48 + 18 + col + ((cx - 18) & 3)
+    uint4* win = s_win[threadIdx.x >> 6][q];
+    {
+        int r = sl / 3, c = sl - 3 * (sl / 3);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if (r < kDescWinRows) win[3 * r + c] = wv4[k];
+            r += 5;
+            c += 1;
+            if (c >= 3) {
+                c -= 3;
+                r += 1;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // rint by the 1.5 * 2^23 trick: the sum's low mantissa bits hold 0x400000 + rint(x); v_mad_u32_u24
     // reads only the low 24 bits, and the biases fold into one per-keypoint constant (mod 2^32)
-    const uint32_t pitch24 = (uint32_t)L.pitch & 0xFFFFFFu;
-    const uint32_t boff = (uint32_t)((cy - 19) * L.pitch + cx - 19) + 19u * pitch24 + 19u - 0x400000u * pitch24 -
-                          __float_as_uint(12582912.0f);
+    const uint8_t* wb = (const uint8_t*)win;
+    const uint32_t woff = 18u * 48u + 18u + (uint32_t)((cx - 18) & 3) - 0x400000u * 48u - __float_as_uint(12582912.0f);
     int val[32];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1341,7 +1382,7 @@ __global__ __launch_bounds__(256) void k_describe(Geo g, const uint8_t* __restri
             const df2 m = (df2){py, py} * (df2){a, -b};
             const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, m) + (df2){12582912.0f, 12582912.0f};
             const uint32_t fr = __float_as_uint(rc.x), fc = __float_as_uint(rc.y);
-            val[2 * i + e] = __builtin_amdgcn_raw_buffer_load_b8(br, (fr & 0xFFFFFFu) * pitch24 + fc + boff, 0, 0);
+            val[2 * i + e] = wb[(fr & 0xFFFFFFu) * 48u + fc + woff];
         }
     }
     uint64_t mine = 0;
