@@ -24,7 +24,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-STAGES = ["resize", "detect", "octree", "describe", "stereo"]
+STAGES = ["resize", "detect", "octree", "blur", "describe", "stereo"]
 
 
 def level_sizes(W, H, nlevels=8, sf=1.2):
@@ -47,6 +47,8 @@ def algorithmic_bytes_per_pair(W, H, N=2000, nlevels=8):
         "detect": 2 * px,
         # the selected keypoints (4 B packed) written and read back
         "octree": 2 * 2 * N * 4,
+        # every level read once and its blurred copy written once
+        "blur": 2 * 2 * px,
         # keypoint records + descriptors written (24 + 32 B per keypoint)
         "describe": 2 * N * 56,
         # both keypoint sets read + uR/depth written
@@ -162,7 +164,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms = (C.c_float * 5)()
+    ms = (C.c_float * len(STAGES))()
     nb = C.c_int32()
     if prof:
         call("orbfe_profile_read", fe.handle, ms, C.byref(nb))

@@ -187,11 +187,12 @@ int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, con
                          int32_t* out);
 
 /* ---- live stage timing --------------------------------------------------------------------------
- * While profiling is on, every batch enqueued on the handle records HIP events on its launch stream
- * at the stage boundaries: 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree,
- * 3 describe (IC angle + blur + BRIEF), 4 stereo.  orbfe_profile_read synchronises and returns the
- * summed milliseconds per stage over the recorded batches. */
-#define ORBFE_NSTAGES 5
+ * While profiling is on, every batch enqueued on the handle records HIP events around its stages:
+ * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 blur (k_blur, timed on the side
+ * stream it runs on, concurrently with detect/octree), 4 describe (IC angle + BRIEF), 5 stereo.
+ * orbfe_profile_read synchronises and returns the summed milliseconds per stage (ms_per_stage holds
+ * ORBFE_NSTAGES floats) over the recorded batches. */
+#define ORBFE_NSTAGES 6
 int orbfe_profile_begin(orbfe_handle h, int32_t max_batches);
 int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches);
 

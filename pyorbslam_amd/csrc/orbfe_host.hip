@@ -36,6 +36,11 @@ inline short sat_short(int v) { return (short)std::min(std::max(v, -32768), 3276
 
 // concurrent chunks of orbfe_frontend_batch_device (the box exposes 4 hardware queues per process)
 constexpr int kLanes = 4;
+// profiling events per batch and the event pair of each stage (resize, detect, octree, blur, describe,
+// stereo); see prof_mark
+constexpr int kProfEvents = 9;
+constexpr int kProfFrom[ORBFE_NSTAGES] = {0, 1, 2, 7, 4, 5};
+constexpr int kProfTo[ORBFE_NSTAGES] = {1, 2, 3, 8, 5, 6};
 
 struct orbfe_ctx {
     orbfe_params prm{};
@@ -80,7 +85,7 @@ struct orbfe_ctx {
     DevBuf<uint8_t> d_hq, d_ht;
     DevBuf<int> d_hoff, d_hidx, d_hres;
 
-    // live profiling: (ORBFE_NSTAGES + 1) events per batch
+    // live profiling: kProfEvents events per batch (see prof_mark)
     std::vector<hipEvent_t> prof_ev;
     int prof_max = 0, prof_n = 0;
     bool prof_on = false;
@@ -416,10 +421,12 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     }
 }
 
-// record boundary `k` (0..ORBFE_NSTAGES) of the current profiled batch
+// record event `k` of the current profiled batch.  Launch stream: 0 start, 1 after resize, 2 after
+// detect, 3 after octree, 4 blur joined (describe starts), 5 after describe, 6 after stereo; the blur
+// stream: 7 before k_blur, 8 after it.  Stage k spans events kProfFrom[k] -> kProfTo[k].
 void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
     if (!c.prof_on || c.prof_n >= c.prof_max) return;
-    HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * (ORBFE_NSTAGES + 1) + k], s));
+    HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * kProfEvents + k], s));
 }
 
 // Images [i0, i0 + n) of the batch: every per-image buffer is passed at the chunk's offset, the
@@ -454,7 +461,9 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
         }
         HIPCK(hipEventRecord(c.ev_fork[k], s));
         HIPCK(hipStreamWaitEvent(c.side_stream[k], c.ev_fork[k], 0));
+        if (prof) prof_mark(c, c.side_stream[k], 7);
         HIPCK(launch_blur(g, in, pitch, ws, blur, n, c.side_stream[k]));
+        if (prof) prof_mark(c, c.side_stream[k], 8);
         HIPCK(hipEventRecord(c.ev_join[k], c.side_stream[k]));
     }
     if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
@@ -462,10 +471,16 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
                         s));
     if (prof) prof_mark(c, s, 3);
-    if (fork_blur) HIPCK(hipStreamWaitEvent(s, c.ev_join[lane + 1], 0));  // join
-    else HIPCK(launch_blur(g, in, pitch, ws, blur, n, s));
-    HIPCK(launch_describe(g, in, pitch, ws, blur, lvl_kp, lvl_count, kps, desc, count, c.d_mw.p, n, s));
+    if (fork_blur) {
+        HIPCK(hipStreamWaitEvent(s, c.ev_join[lane + 1], 0));  // join
+    } else {
+        if (prof) prof_mark(c, s, 7);
+        HIPCK(launch_blur(g, in, pitch, ws, blur, n, s));
+        if (prof) prof_mark(c, s, 8);
+    }
     if (prof) prof_mark(c, s, 4);
+    HIPCK(launch_describe(g, in, pitch, ws, blur, lvl_kp, lvl_count, kps, desc, count, c.d_mw.p, n, s));
+    if (prof) prof_mark(c, s, 5);
 }
 
 void check_extract(orbfe_ctx& c, int64_t pitch, int n) {
@@ -536,7 +551,7 @@ void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStr
     stereo_range(c, c.last_in, c.last_pitch, 0, n_pairs, bf, fx, s);
     c.last_bf = bf;
     c.last_fx = fx;
-    prof_mark(c, s, 5);
+    prof_mark(c, s, 6);
     if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
     c.last_pairs = n_pairs;
 }
@@ -553,7 +568,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     if (K == 1) {
         extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true, true);
         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
-        prof_mark(c, s, 5);
+        prof_mark(c, s, 6);
     } else {
         if (!c.lane_stream[0]) {
             for (int k = 0; k < kLanes; ++k) {
@@ -569,7 +584,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
             extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, true, k);
             stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
-            if (k == 0) prof_mark(c, ls, 5);
+            if (k == 0) prof_mark(c, ls, 6);
             HIPCK(hipEventRecord(c.lane_done[k], ls));
         }
         for (int k = 0; k < K; ++k) HIPCK(hipStreamWaitEvent(s, c.lane_done[k], 0));
@@ -908,7 +923,7 @@ int orbfe_hamming_csr(orbfe_handle h, const uint8_t* query_desc, int32_t n_query
 int orbfe_profile_begin(orbfe_handle h, int32_t max_batches) {
     return guarded([&] {
         if (!h || max_batches < 0) throw Error(ORBFE_EINVAL, "bad argument");
-        const size_t need = (size_t)max_batches * (ORBFE_NSTAGES + 1);
+        const size_t need = (size_t)max_batches * kProfEvents;
         while (h->prof_ev.size() < need) {
             hipEvent_t e;
             HIPCK(hipEventCreate(&e));
@@ -925,11 +940,12 @@ int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches) 
         if (!h || !ms_per_stage) throw Error(ORBFE_EINVAL, "null argument");
         for (int k = 0; k < ORBFE_NSTAGES; ++k) ms_per_stage[k] = 0.f;
         for (int b = 0; b < h->prof_n; ++b) {
-            hipEvent_t* e = &h->prof_ev[(size_t)b * (ORBFE_NSTAGES + 1)];
-            HIPCK(hipEventSynchronize(e[ORBFE_NSTAGES]));
+            hipEvent_t* e = &h->prof_ev[(size_t)b * kProfEvents];
+            HIPCK(hipEventSynchronize(e[6]));
+            HIPCK(hipEventSynchronize(e[8]));
             for (int k = 0; k < ORBFE_NSTAGES; ++k) {
                 float ms = 0.f;
-                HIPCK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+                HIPCK(hipEventElapsedTime(&ms, e[kProfFrom[k]], e[kProfTo[k]]));
                 ms_per_stage[k] += ms;
             }
         }
