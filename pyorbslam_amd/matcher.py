@@ -1,8 +1,10 @@
-"""Drop-in for the reference ORBMatcher's Hamming searches (ORBMatcher.py).
+"""Drop-in for the reference ORBMatcher (ORBMatcher.py): every search of the class.
 
-descriptor_distance (ORBMatcher.py:12-14), search_by_projection_f_p (:215-283) and
-search_by_projection_f_f (:291-393) keep the reference's control flow and results exactly; what changes
-is where the popcounts happen.  The reference calls a per-byte Python popcount (~10 us) once per
+descriptor_distance (ORBMatcher.py:12-14), the BoW searches search_by_BoW_kf_f / _kf_kf (:21-213), the
+projection searches search_by_projection_f_p / _f_f / _ckf_scw_mp / _f_kf_f (:215-393, 850-1008), the
+fusions fuse_kf_scw_mp / fuse_pkf_mp (:395-582), search_for_triangulation (:584-711) and search_by_sim3
+(:713-848) keep the reference's control flow and results exactly; what changes is where the popcounts
+happen.  The reference calls a per-byte Python popcount (~10 us) once per
 candidate inside the search loop.  Here every (query, candidate) pair of a search is collected first —
 the candidate windows depend only on the frame grid, never on matches made during the search — and
 all distances come back from ONE k_hamming_search launch (orbfe_hamming_csr).  The sequential part
@@ -10,6 +12,14 @@ that genuinely depends on earlier iterations (candidates already holding a map p
 observations, the stereo gate, best / second-best bookkeeping, the rotation histogram) then runs on the
 host over those precomputed distances, evaluating the same Python expressions on the same objects, so
 every dtype promotion of the reference is preserved.
+
+The split into "collect, then replay" is exact because everything the collection phase evaluates is
+static during a search (keypoints, grids, poses, map-point geometry, map-point badness at collection
+time — badness never reverts), while every piece of state a search mutates (matched slots, keyframe
+map-point slots, observations) is read in the replay phase at the reference's point in the loop.  The one
+input a search can change under itself is a map point's descriptor (fuse_pkf_mp: MapPoint.replace
+recomputes the survivor's distinctive descriptor, MapPoint.py:180); the replay compares the descriptor it
+reads with the collected one and re-runs that query's distances on the GPU when they differ.
 """
 from __future__ import annotations
 
@@ -217,4 +227,562 @@ class ORBMatcher:
                     for idx in rot_hist[i]:
                         current_frame.mvpMapPoints[idx] = None
                         n_matches -= 1
+        return n_matches
+
+    # ------------------------------------------------------------------------------------------------
+    # helpers shared by the keyframe-level searches
+
+    def _reject_by_rotation(self, rot_hist, on_reject):
+        """Keep the three fullest rotation bins (ORBMatcher.py:16-19 + the callers' loops)."""
+        ind1, ind2, ind3 = self.compute_three_maxima(rot_hist, HISTO_LENGTH)
+        n = 0
+        for i in range(HISTO_LENGTH):
+            if i in [ind1, ind2, ind3]:
+                continue
+            for idx in rot_hist[i]:
+                on_reject(idx)
+                n += 1
+        return n
+
+    @staticmethod
+    def _bow_common_nodes(fv1, fv2):
+        """Nodes present in both DBoW2 feature vectors, in the order the reference's merge walk visits
+        them (ORBMatcher.py:39-103, 140-196: advance both on equal keys, else the smaller one)."""
+        out = []
+        it1, it2 = iter(fv1), iter(fv2)
+        try:
+            k1 = next(it1)
+            k2 = next(it2)
+            while True:
+                if k1 == k2:
+                    out.append(k1)
+                    k1 = next(it1)
+                    k2 = next(it2)
+                elif k1 < k2:
+                    k1 = next(it1)
+                else:
+                    k2 = next(it2)
+        except StopIteration:
+            pass
+        return out
+
+    def _query_dists(self, pMP, snap, cands, dq, train):
+        """Distances of a query collected earlier; re-run on the GPU if its descriptor changed since."""
+        d = pMP.get_descriptor()
+        if np.array_equal(np.asarray(d).reshape(-1), np.asarray(snap).reshape(-1)):
+            return dq
+        return self._batched([(d, cands)], train)[0]
+
+    # ORBMatcher.py:21-118
+    def search_by_BoW_kf_f(self, kf, frame):
+        vpMapPointsKF = kf.get_map_point_matches()
+        vpMapPointMatches = [None] * frame.N
+        fv_kf, fv_f = kf.mFeatVec, frame.mFeatVec
+        n_matches = 0
+        rot_hist = [[] for _ in range(HISTO_LENGTH)]
+        factor = 1.0 / HISTO_LENGTH
+        work = []
+        for node in self._bow_common_nodes(fv_kf, fv_f):
+            cands = fv_f[node]
+            for idx_kf in fv_kf[node]:
+                pMP = vpMapPointsKF[idx_kf]
+                if not pMP or pMP.is_bad():
+                    continue
+                work.append((idx_kf, pMP, cands, kf.mDescriptors[idx_kf]))
+        dists = self._batched([(w[3], w[2]) for w in work], frame.mDescriptors)
+        for (idx_kf, pMP, cands, _), dq in zip(work, dists):
+            best1, best_idx, best2 = 256, -1, 256
+            for idx_f, dist in zip(cands, dq.tolist()):
+                if vpMapPointMatches[idx_f]:
+                    continue
+                if dist < best1:
+                    best2 = best1
+                    best1 = dist
+                    best_idx = idx_f
+                elif dist < best2:
+                    best2 = dist
+            if best1 <= TH_LOW and float(best1) < self.mfNNratio * float(best2):
+                vpMapPointMatches[best_idx] = pMP
+                kp = kf.mvKeysUn[idx_kf]
+                if self.mbCheckOrientation:
+                    rot = kp.angle - frame.mvKeys[best_idx].angle
+                    if rot < 0.0:
+                        rot += 360.0
+                    b = round(rot * factor)
+                    if b == HISTO_LENGTH:
+                        b = 0
+                    assert 0 <= b < HISTO_LENGTH
+                    rot_hist[b].append(best_idx)
+                n_matches += 1
+        if self.mbCheckOrientation:
+            n_matches -= self._reject_by_rotation(rot_hist, lambda i: vpMapPointMatches.__setitem__(i, None))
+        return n_matches, vpMapPointMatches
+
+    # ORBMatcher.py:120-213
+    def search_by_BoW_kf_kf(self, pKF1, pKF2):
+        vKeysUn1, vKeysUn2 = pKF1.mvKeysUn, pKF2.mvKeysUn
+        fv1, fv2 = pKF1.mFeatVec, pKF2.mFeatVec
+        vpMapPoints1 = pKF1.get_map_point_matches()
+        vpMapPoints2 = pKF2.get_map_point_matches()
+        vpMatches12 = [None] * len(vpMapPoints1)
+        vbMatched2 = [False] * len(vpMapPoints2)
+        rot_hist = [[] for _ in range(HISTO_LENGTH)]
+        factor = 1.0 / HISTO_LENGTH
+        n_matches = 0
+        work = []
+        for node in self._bow_common_nodes(fv1, fv2):
+            cands = []
+            for idx2 in fv2[node]:
+                pMP2 = vpMapPoints2[idx2]
+                if not pMP2 or pMP2.is_bad():
+                    continue
+                cands.append(idx2)
+            for idx1 in fv1[node]:
+                pMP1 = vpMapPoints1[idx1]
+                if not pMP1 or pMP1.is_bad():
+                    continue
+                work.append((idx1, cands, pKF1.mDescriptors[idx1]))
+        dists = self._batched([(w[2], w[1]) for w in work], pKF2.mDescriptors)
+        for (idx1, cands, _), dq in zip(work, dists):
+            best1, best_idx2, best2 = 256, -1, 256
+            for idx2, dist in zip(cands, dq.tolist()):
+                if vbMatched2[idx2]:
+                    continue
+                if dist < best1:
+                    best2 = best1
+                    best1 = dist
+                    best_idx2 = idx2
+                elif dist < best2:
+                    best2 = dist
+            if best1 < TH_LOW and best1 < self.mfNNratio * best2:
+                vpMatches12[idx1] = vpMapPoints2[best_idx2]
+                vbMatched2[best_idx2] = True
+                if self.mbCheckOrientation:
+                    rot = vKeysUn1[idx1].angle - vKeysUn2[best_idx2].angle
+                    if rot < 0.0:
+                        rot += 360.0
+                    b = round(rot * factor)
+                    if b == HISTO_LENGTH:
+                        b = 0
+                    rot_hist[b].append(idx1)
+                n_matches += 1
+        if self.mbCheckOrientation:
+            n_matches -= self._reject_by_rotation(rot_hist, lambda i: vpMatches12.__setitem__(i, None))
+        return n_matches, vpMatches12
+
+    @staticmethod
+    def _sim3_to_pose(Scw):
+        sRcw = Scw[:3, :3]
+        scw = np.sqrt(np.dot(sRcw[0], sRcw[0]))
+        Rcw = sRcw / scw
+        tcw = Scw[:3, 3:4] / scw
+        return Rcw, tcw, -Rcw.T @ tcw
+
+    @staticmethod
+    def _project_checked(pMP, pKF, Rcw, tcw, strict_z):
+        """Camera projection of fuse_kf_scw_mp (:414-427, strict_z False) and
+        search_by_projection_ckf_scw_mp (:868-878, strict_z True: `<= 0` and 1-element array
+        arithmetic, as there).  Returns (u, v, invz, p3Dw) or None."""
+        p3Dw = pMP.get_world_pos()
+        p3Dc = Rcw @ p3Dw + tcw
+        if strict_z:
+            if p3Dc[2][0] <= 0.0:
+                return None
+            invz = 1.0 / p3Dc[2]
+            x, y = p3Dc[0] * invz, p3Dc[1] * invz
+        else:
+            if p3Dc[2][0] < 0.0:
+                return None
+            invz = 1.0 / p3Dc[2][0]
+            x = p3Dc[0][0] * invz
+            y = p3Dc[1][0] * invz
+        u = pKF.fx * x + pKF.cx
+        v = pKF.fy * y + pKF.cy
+        return u, v, invz, p3Dw
+
+    @staticmethod
+    def _distance_gates(pMP, pKF, p3Dw, Ow):
+        """Scale-invariance distance and viewing-angle gates (:429-441); the predicted level or None."""
+        maxDistance = pMP.get_max_distance_invariance()
+        minDistance = pMP.get_min_distance_invariance()
+        PO = p3Dw - Ow
+        dist3D = np.linalg.norm(PO)
+        if dist3D < minDistance or dist3D > maxDistance:
+            return None
+        Pn = pMP.get_normal()
+        if np.dot(PO.T, Pn) < 0.5 * dist3D:
+            return None
+        return pMP.predict_scale(dist3D, pKF)
+
+    # ORBMatcher.py:395-480
+    def fuse_kf_scw_mp(self, pKF, Scw, vpPoints, th, vpReplacePoint):
+        Rcw, tcw, Ow = self._sim3_to_pose(Scw)
+        spAlreadyFound = pKF.get_map_points()
+        work = []
+        for iMP, pMP in enumerate(vpPoints):
+            if pMP.is_bad() or pMP in spAlreadyFound:
+                continue
+            pr = self._project_checked(pMP, pKF, Rcw, tcw, False)
+            if pr is None:
+                continue
+            u, v, _, p3Dw = pr
+            if not pKF.is_in_image(u, v):
+                continue
+            lvl = self._distance_gates(pMP, pKF, p3Dw, Ow)
+            if lvl is None:
+                continue
+            vIndices = pKF.get_features_in_area(u, v, th * pKF.mvScaleFactors[lvl])
+            if not vIndices:
+                continue
+            cands = [i for i in vIndices if lvl - 1 <= pKF.mvKeysUn[i].octave <= lvl]
+            work.append((iMP, pMP, cands, pMP.get_descriptor()))
+        dists = self._batched([(w[3], w[2]) for w in work], pKF.mDescriptors)
+        n_fused = 0
+        for (iMP, pMP, cands, _), dq in zip(work, dists):
+            best_dist, best_idx = float('inf'), -1
+            for idx, dist in zip(cands, dq.tolist()):
+                if dist < best_dist:
+                    best_dist = dist
+                    best_idx = idx
+            if best_dist <= TH_LOW:
+                pMPinKF = pKF.get_map_point(best_idx)
+                if pMPinKF:
+                    if not pMPinKF.is_bad():
+                        vpReplacePoint[iMP] = pMPinKF
+                else:
+                    pMP.add_observation(pKF, best_idx)
+                    pKF.add_map_point(pMP, best_idx)
+                n_fused += 1
+        return n_fused, vpReplacePoint
+
+    # ORBMatcher.py:482-582
+    def fuse_pkf_mp(self, pKF, vpMapPoints, th):
+        fx, fy, cx, cy, bf = pKF.fx, pKF.fy, pKF.cx, pKF.cy, pKF.mbf
+        Rcw = pKF.get_rotation()
+        tcw = pKF.get_translation()
+        Ow = pKF.get_camera_center()
+        work = []
+        for pMP in vpMapPoints:
+            # badness never reverts, so a point bad now is skipped by the replay as well; whether it is in
+            # the keyframe can change during the search and is checked there
+            if not pMP or pMP.is_bad():
+                continue
+            p3Dw = pMP.get_world_pos()
+            p3Dc = Rcw @ p3Dw + tcw
+            if p3Dc[2][0] < 0.0:
+                continue
+            invz = 1.0 / p3Dc[2][0]
+            x = p3Dc[0][0] * invz
+            y = p3Dc[1][0] * invz
+            u = fx * x + cx
+            v = fy * y + cy
+            ur = u - bf * invz
+            if not pKF.is_in_image(u, v):
+                continue
+            lvl = self._distance_gates(pMP, pKF, p3Dw, Ow)
+            if lvl is None:
+                continue
+            vIndices = pKF.get_features_in_area(u, v, th * pKF.mvScaleFactors[lvl])
+            if not vIndices:
+                continue
+            cands = []
+            for idx in vIndices:
+                kp = pKF.mvKeysUn[idx]
+                kpLevel = kp.octave
+                if kpLevel < lvl - 1 or kpLevel > lvl:
+                    continue
+                if pKF.mvuRight[idx] >= 0:
+                    ex, ey, er = u - kp.pt[0], v - kp.pt[1], ur - pKF.mvuRight[idx]
+                    if (ex ** 2 + ey ** 2 + er ** 2) * pKF.mvInvLevelSigma2[kpLevel] > 7.8:
+                        continue
+                else:
+                    ex, ey = u - kp.pt[0], v - kp.pt[1]
+                    if (ex ** 2 + ey ** 2) * pKF.mvInvLevelSigma2[kpLevel] > 5.99:
+                        continue
+                cands.append(idx)
+            work.append((pMP, cands, pMP.get_descriptor()))
+        dists = self._batched([(w[2], w[1]) for w in work], pKF.mDescriptors)
+        n_fused = 0
+        for (pMP, cands, snap), dq in zip(work, dists):
+            if pMP.is_bad() or pMP.is_in_key_frame(pKF):
+                continue
+            dq = self._query_dists(pMP, snap, cands, dq, pKF.mDescriptors)
+            best_dist, best_idx = float('inf'), -1
+            for idx, dist in zip(cands, dq.tolist()):
+                if dist < best_dist:
+                    best_dist = dist
+                    best_idx = idx
+            if best_dist <= TH_LOW:
+                pMPinKF = pKF.get_map_point(best_idx)
+                if pMPinKF:
+                    if not pMPinKF.is_bad():
+                        if pMPinKF.observations() > pMP.observations():
+                            pMP.replace(pMPinKF)
+                        else:
+                            pMPinKF.replace(pMP)
+                else:
+                    pMP.add_observation(pKF, best_idx)
+                    pKF.add_map_point(pMP, best_idx)
+                n_fused += 1
+        return n_fused
+
+    @staticmethod
+    def _triangulation_nodes(fv1, fv2):
+        """The node pairs search_for_triangulation visits (ORBMatcher.py:606-675).  Its walk draws a
+        fresh item from both vectors every round and, on unequal keys, discards one more item of the
+        smaller side — outside the try block, so an exhausted vector there raises StopIteration out of
+        the search.  Reproduced as is (the search has no side effects before that point)."""
+        out = []
+        it1, it2 = iter(fv1.items()), iter(fv2.items())
+        while True:
+            try:
+                k1, v1 = next(it1)
+                k2, v2 = next(it2)
+            except StopIteration:
+                break
+            if k1 == k2:
+                out.append((v1, v2))
+            elif k1 < k2:
+                next(it1)
+            else:
+                next(it2)
+        return out
+
+    # ORBMatcher.py:584-696
+    def search_for_triangulation(self, pKF1, pKF2, F12, bOnlyStereo=False):
+        Cw = pKF1.get_camera_center()
+        R2w = pKF2.get_rotation()
+        t2w = pKF2.get_translation()
+        C2 = R2w @ Cw + t2w
+        invz = 1.0 / C2[2]
+        ex = pKF2.fx * C2[0] * invz + pKF2.cx
+        ey = pKF2.fy * C2[1] * invz + pKF2.cy
+        vbMatched2 = [False] * pKF2.N
+        vMatches12 = [-1] * pKF1.N
+        rot_hist = [[] for _ in range(HISTO_LENGTH)]
+        factor = 1.0 / HISTO_LENGTH
+        n_matches = 0
+        work = []
+        for f1val, f2val in self._triangulation_nodes(pKF1.mFeatVec, pKF2.mFeatVec):
+            cands = []
+            for idx2 in f2val:
+                if pKF2.get_map_point(idx2):
+                    continue
+                bStereo2 = pKF2.mvuRight[idx2] >= 0
+                if bOnlyStereo and not bStereo2:
+                    continue
+                cands.append((idx2, bStereo2))
+            for idx1 in f1val:
+                if pKF1.get_map_point(idx1):
+                    continue
+                bStereo1 = pKF1.mvuRight[idx1] >= 0
+                if bOnlyStereo and not bStereo1:
+                    continue
+                work.append((idx1, bStereo1, cands, pKF1.mDescriptors[idx1]))
+        dists = self._batched([(w[3], [c[0] for c in w[2]]) for w in work], pKF2.mDescriptors)
+        for (idx1, bStereo1, cands, _), dq in zip(work, dists):
+            kp1 = pKF1.mvKeysUn[idx1]
+            best_dist, best_idx2 = TH_LOW, -1
+            for (idx2, bStereo2), dist in zip(cands, dq.tolist()):
+                if vbMatched2[idx2]:
+                    continue
+                if dist > TH_LOW or dist > best_dist:
+                    continue
+                kp2 = pKF2.mvKeysUn[idx2]
+                if not bStereo1 and not bStereo2:
+                    distex = ex - kp2.pt[0]
+                    distey = ey - kp2.pt[1]
+                    if distex ** 2 + distey ** 2 < 100 * pKF2.mvScaleFactors[kp2.octave]:
+                        continue
+                if self.check_dist_epipolar_line(kp1, kp2, F12, pKF2):
+                    best_idx2 = idx2
+                    best_dist = dist
+            if best_idx2 >= 0:
+                kp2 = pKF2.mvKeysUn[best_idx2]
+                vMatches12[idx1] = best_idx2
+                n_matches += 1
+                vbMatched2[best_idx2] = True
+                if self.mbCheckOrientation:
+                    rot = kp1.angle - kp2.angle
+                    if rot < 0:
+                        rot += 360.0
+                    b = round(rot * factor)
+                    if b == HISTO_LENGTH:
+                        b = 0
+                    rot_hist[b].append(idx1)
+        if self.mbCheckOrientation:
+            n_matches -= self._reject_by_rotation(rot_hist, lambda i: vMatches12.__setitem__(i, -1))
+        return [(i, m) for i, m in enumerate(vMatches12) if m >= 0]
+
+    # ORBMatcher.py:698-711
+    def check_dist_epipolar_line(self, kp1, kp2, F12, pKF2):
+        a = kp1.pt[0] * F12[0, 0] + kp1.pt[1] * F12[1, 0] + F12[2, 0]
+        b = kp1.pt[0] * F12[0, 1] + kp1.pt[1] * F12[1, 1] + F12[2, 1]
+        c = kp1.pt[0] * F12[0, 2] + kp1.pt[1] * F12[1, 2] + F12[2, 2]
+        num = a * kp2.pt[0] + b * kp2.pt[1] + c
+        den = a ** 2 + b ** 2
+        if den == 0:
+            return False
+        return (num ** 2) / den < 3.84 * pKF2.mvLevelSigma2[kp2.octave]
+
+    def _sim3_side(self, vpMapPoints, already, Rw, tw, sR, t, pKFo, th, K):
+        """One direction of search_by_sim3 (ORBMatcher.py:744-783 / 785-825): best index in pKFo per point.
+        K = (fx, fy, cx, cy): the reference projects both directions with pKF1's intrinsics."""
+        fx, fy, cx, cy = K
+        work = []
+        for i, pMP in enumerate(vpMapPoints):
+            if not pMP or already[i] or pMP.is_bad():
+                continue
+            p3Dw = pMP.get_world_pos()
+            p3Dc = sR @ (Rw @ p3Dw + tw) + t
+            if p3Dc[2] < 0.0:
+                continue
+            invz = 1.0 / p3Dc[2]
+            x, y = p3Dc[0] * invz, p3Dc[1] * invz
+            u, v = fx * x + cx, fy * y + cy
+            if not pKFo.is_in_image(u, v):
+                continue
+            maxDistance = pMP.get_max_distance_invariance()
+            minDistance = pMP.get_min_distance_invariance()
+            dist3D = np.linalg.norm(p3Dc)
+            if not (minDistance <= dist3D <= maxDistance):
+                continue
+            lvl = pMP.predict_scale(dist3D, pKFo)
+            vIndices = pKFo.get_features_in_area(u, v, th * pKFo.mvScaleFactors[lvl])
+            if not vIndices:
+                continue
+            cands = [idx for idx in vIndices if lvl - 1 <= pKFo.mvKeysUn[idx].octave <= lvl]
+            work.append((i, cands, pMP.get_descriptor()))
+        best = [-1] * len(vpMapPoints)
+        for (i, cands, _), dq in zip(work, self._batched([(w[2], w[1]) for w in work], pKFo.mDescriptors)):
+            best_dist, best_idx = np.inf, -1
+            for idx, dist in zip(cands, dq.tolist()):
+                if dist < best_dist:
+                    best_dist, best_idx = dist, idx
+            if best_dist <= TH_HIGH:
+                best[i] = best_idx
+        return best
+
+    # ORBMatcher.py:713-848
+    def search_by_sim3(self, pKF1, pKF2, vpMatches12, s12, R12, t12, th):
+        R1w, t1w = pKF1.get_rotation(), pKF1.get_translation()
+        R2w, t2w = pKF2.get_rotation(), pKF2.get_translation()
+        sR12 = s12 * R12
+        sR21 = (1.0 / s12) * R12.T
+        t21 = -sR21 @ t12
+        vpMapPoints1 = pKF1.get_map_point_matches()
+        vpMapPoints2 = pKF2.get_map_point_matches()
+        N1, N2 = len(vpMapPoints1), len(vpMapPoints2)
+        vbAlreadyMatched1 = [False] * N1
+        vbAlreadyMatched2 = [False] * N2
+        for i, pMP in enumerate(vpMatches12):
+            if pMP:
+                vbAlreadyMatched1[i] = True
+                idx2 = pMP.get_index_in_keyframe(pKF2)
+                if 0 <= idx2 < N2:
+                    vbAlreadyMatched2[idx2] = True
+        K = (pKF1.fx, pKF1.fy, pKF1.cx, pKF1.cy)
+        vnMatch1 = self._sim3_side(vpMapPoints1, vbAlreadyMatched1, R1w, t1w, sR21, t21, pKF2, th, K)
+        vnMatch2 = self._sim3_side(vpMapPoints2, vbAlreadyMatched2, R2w, t2w, sR12, t12, pKF1, th, K)
+        n_found = 0
+        for i1, idx2 in enumerate(vnMatch1):
+            if idx2 >= 0 and vnMatch2[idx2] == i1:
+                vpMatches12[i1] = vpMapPoints2[idx2]
+                n_found += 1
+        return n_found, vpMatches12
+
+    # ORBMatcher.py:850-922
+    def search_by_projection_ckf_scw_mp(self, pKF, Scw, vpPoints, vpMatched, th):
+        sRcw = Scw[:3, :3]
+        scw = np.linalg.norm(sRcw[0])
+        Rcw = sRcw / scw
+        tcw = Scw[:3, 3:4] / scw
+        Ow = -Rcw.T @ tcw
+        spAlreadyFound = set(vpMatched) - {None}
+        work = []
+        for pMP in vpPoints:
+            if pMP.is_bad() or pMP in spAlreadyFound:
+                continue
+            pr = self._project_checked(pMP, pKF, Rcw, tcw, True)
+            if pr is None:
+                continue
+            u, v, _, p3Dw = pr
+            if not pKF.is_in_image(u, v):
+                continue
+            lvl = self._distance_gates(pMP, pKF, p3Dw, Ow)
+            if lvl is None:
+                continue
+            vIndices = pKF.get_features_in_area(u, v, th * pKF.mvScaleFactors[lvl])
+            if not vIndices:
+                continue
+            cands = [i for i in vIndices if lvl - 1 <= pKF.mvKeysUn[i].octave <= lvl]
+            work.append((pMP, cands, pMP.get_descriptor()))
+        n_matches = 0
+        for (pMP, cands, _), dq in zip(work, self._batched([(w[2], w[1]) for w in work], pKF.mDescriptors)):
+            best_dist, best_idx = 256, -1
+            for idx, dist in zip(cands, dq.tolist()):
+                if vpMatched[idx] is not None:
+                    continue
+                if dist < best_dist:
+                    best_dist = dist
+                    best_idx = idx
+            if best_dist <= TH_LOW:
+                vpMatched[best_idx] = pMP
+                n_matches += 1
+        return n_matches, vpMatched
+
+    # ORBMatcher.py:924-1008
+    def search_by_projection_f_kf_f(self, CurrentFrame, pKF, sAlreadyFound, th, ORBdist):
+        Rcw = CurrentFrame.mTcw[:3, :3]
+        tcw = CurrentFrame.mTcw[:3, 3:4]
+        Ow = -np.dot(Rcw.T, tcw)
+        rot_hist = [[] for _ in range(HISTO_LENGTH)]
+        factor = 1.0 / HISTO_LENGTH
+        work = []
+        for i, pMP in enumerate(pKF.get_map_point_matches()):
+            if not (pMP and not pMP.is_bad() and pMP not in sAlreadyFound):
+                continue
+            x3Dw = pMP.get_world_pos()
+            x3Dc = np.dot(Rcw, x3Dw) + tcw
+            invzc = 1.0 / x3Dc[2]
+            u = CurrentFrame.fx * x3Dc[0] * invzc + CurrentFrame.cx
+            v = CurrentFrame.fy * x3Dc[1] * invzc + CurrentFrame.cy
+            if u < CurrentFrame.mnMinX or u > CurrentFrame.mnMaxX or v < CurrentFrame.mnMinY or v > CurrentFrame.mnMaxY:
+                continue
+            PO = x3Dw - Ow
+            dist3D = np.linalg.norm(PO)
+            maxDistance = pMP.get_max_distance_invariance()
+            minDistance = pMP.get_min_distance_invariance()
+            if dist3D < minDistance or dist3D > maxDistance:
+                continue
+            lvl = pMP.predict_scale(dist3D, CurrentFrame)
+            vIndices2 = CurrentFrame.get_features_in_area(u, v, th * CurrentFrame.mvScaleFactors[lvl], lvl - 1, lvl + 1)
+            if not vIndices2:
+                continue
+            work.append((i, pMP, vIndices2, pMP.get_descriptor()))
+        n_matches = 0
+        for (i, pMP, cands, _), dq in zip(work, self._batched([(w[3], w[2]) for w in work],
+                                                             CurrentFrame.mDescriptors)):
+            best_dist, best_idx2 = 256, -1
+            for i2, dist in zip(cands, dq.tolist()):
+                if CurrentFrame.mvpMapPoints[i2]:
+                    continue
+                if dist < best_dist:
+                    best_dist = dist
+                    best_idx2 = i2
+            if best_dist <= ORBdist:
+                CurrentFrame.mvpMapPoints[best_idx2] = pMP
+                n_matches += 1
+                if self.mbCheckOrientation:
+                    rot = pKF.mvKeysUn[i].angle - CurrentFrame.mvKeysUn[best_idx2].angle
+                    if rot < 0.0:
+                        rot += 360.0
+                    b = round(rot * factor)
+                    if b == HISTO_LENGTH:
+                        b = 0
+                    assert 0 <= b < HISTO_LENGTH
+                    rot_hist[b].append(best_idx2)
+        if self.mbCheckOrientation:
+            n_matches -= self._reject_by_rotation(rot_hist,
+                                                  lambda i: CurrentFrame.mvpMapPoints.__setitem__(i, None))
         return n_matches
