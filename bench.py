@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--streams", type=int, default=4,
                     help="independent front-end handles per GPU, each on its own stream with P/streams pairs")
     ap.add_argument("--lanes", type=int, default=1, help="internal concurrent chunks per handle (orbfe_set_lanes)")
+    ap.add_argument("--blur-fork", type=int, default=0,
+                    help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles
+                         already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
     ap.add_argument("--cpu-sample", type=int, default=64, help="pairs timed for cpu_baseline (0 = skip; 64 is about 15 s)")
     ap.add_argument("--check", action="store_true", help="verify the last step's pair 0 against the oracle")
     ap.add_argument("--gather", action="store_true",
@@ -137,7 +140,8 @@ def main():
     images = torch.from_numpy(host).to(dev)
     # S sub-batches of P/S pairs, each with its own handle (buffers) and stream, so that the latency-bound
     # stages of one overlap the issue-bound stages of another; every pair is still processed exactly once
-    fes = [StereoFrontEnd(args.width, args.height, max_pairs=P // S, nfeatures=args.nfeatures, lanes=args.lanes)
+    fes = [StereoFrontEnd(args.width, args.height, max_pairs=P // S, nfeatures=args.nfeatures, lanes=args.lanes,
+                          blur_fork=bool(args.blur_fork))
            for _ in range(S)]
     fe = fes[0]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
@@ -218,7 +222,8 @@ def main():
             "config": {"workload": workload, "pairs_per_step_per_gpu": P, "width": args.width,
                        "height": args.height, "nfeatures": args.nfeatures, "nlevels": 8, "scaleFactor": 1.2,
                        "iniThFAST": 20, "minThFAST": 7, "parallelism": f"pairs sharded {world}-way (replicas)",
-                       "handles_per_gpu": S, "lanes_per_handle": args.lanes},
+                       "handles_per_gpu": S, "lanes_per_handle": args.lanes,
+                       "blur_side_stream": bool(args.blur_fork)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),

@@ -134,6 +134,11 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
  * their layout do not depend on it. */
 int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
 
+/* orbfe_set_blur_fork: run k_blur on an internal side stream, concurrently with FAST and the octree
+ * (on = 1, default), or in order on the launch stream (on = 0: one stream per handle, for callers that
+ * already run several handles on their own streams).  Results do not depend on it. */
+int orbfe_set_blur_fork(orbfe_handle h, int32_t on);
+
 /* Device result layout of the last batch (pointers into handle-owned device memory):
  *   kps   : n_images x cap  orbfe_keypoint   (cap = *kp_cap)
  *   desc  : n_images x cap x 32 u8

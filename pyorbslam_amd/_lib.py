@@ -73,6 +73,7 @@ SIGNATURES = {
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
     "orbfe_set_lanes": [C.c_void_p, C.c_int32],
+    "orbfe_set_blur_fork": [C.c_void_p, C.c_int32],
     "orbfe_vocab_load_text": [C.c_char_p, C.POINTER(C.c_void_p)],
     "orbfe_vocab_create": [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_void_p, C.POINTER(C.c_void_p)],

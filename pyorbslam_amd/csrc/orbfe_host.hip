@@ -97,6 +97,7 @@ struct orbfe_ctx {
     hipEvent_t ev_fork[kLanes + 1] = {}, ev_join[kLanes + 1] = {};
     // orbfe_frontend_batch_device: up to kLanes concurrent chunks of the batch on internal streams
     int lanes = kLanes;  // orbfe_set_lanes
+    bool blur_fork = true;  // orbfe_set_blur_fork
     hipStream_t lane_stream[kLanes] = {};
     hipEvent_t lane_done[kLanes] = {};
     hipEvent_t lane_fork = nullptr;
@@ -493,7 +494,7 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     if (n <= 0) return;
     check_extract(c, pitch, n);
     HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
-    extract_range(c, d_in, pitch, 0, n, s, true, true);
+    extract_range(c, d_in, pitch, 0, n, s, true, c.blur_fork);
     c.last_in = d_in;
     c.last_pitch = pitch;
     c.last_images = n;
@@ -566,7 +567,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
     const int K = std::max(1, std::min(c.lanes, n_pairs));
     if (K == 1) {
-        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true, true);
+        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true, c.blur_fork);
         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
         prof_mark(c, s, 6);
     } else {
@@ -582,7 +583,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             const int p0 = (int)((int64_t)n_pairs * k / K), p1 = (int)((int64_t)n_pairs * (k + 1) / K);
             hipStream_t ls = c.lane_stream[k];
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
-            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, true, k);
+            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, c.blur_fork, k);
             stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
             if (k == 0) prof_mark(c, ls, 6);
             HIPCK(hipEventRecord(c.lane_done[k], ls));
@@ -789,6 +790,13 @@ int orbfe_set_lanes(orbfe_handle h, int32_t lanes) {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
         if (lanes < 1 || lanes > kLanes) throw Error(ORBFE_EINVAL, "lanes must be 1..4");
         h->lanes = lanes;
+    });
+}
+
+int orbfe_set_blur_fork(orbfe_handle h, int32_t on) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        h->blur_fork = on != 0;
     });
 }
 

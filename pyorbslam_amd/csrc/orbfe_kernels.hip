@@ -65,6 +65,17 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const u
     return ws + (int64_t)img * g.ws_bytes + g.lv[l].ws_off;
 }
 
+// XCD-aware remap of a (gridDim.x, gridDim.y) grid.  Hardware block i (flattened, x fastest) runs on
+// XCD i % 8; the remap hands each XCD a contiguous run of logical blocks, so neighbouring tiles / cells /
+// bands — which share halo rows and partly used cache lines — meet in the same L2 instead of being
+// fetched from HBM by several XCDs.  Wave-uniform results (SGPRs).
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x, per = nb >> 3;
+    const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;
+    by = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
+    bx = __builtin_amdgcn_readfirstlane(lb - by * (int)gridDim.x);
+}
+
 // Block-wide exclusive scan of a[0..n) in LDS, in place; returns the total.  The first 256 threads own
 // contiguous chunks, so prefixes follow array order; further threads (blocks of up to 1024) only take
 // part in the barriers.  tmp: 257 ints of LDS.
@@ -141,8 +152,10 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     uint32_t* s_src = s_ry + 4 * kRsRows;                // staged source rows
     const LevelGeo& L = g.lv[l];
     const LevelGeo& P = g.lv[l - 1];
-    const int img = blockIdx.y, t = threadIdx.x;
-    const int dy0 = blockIdx.x * kRsRows, nrow = min(kRsRows, L.h - dy0);
+    int bx, img;
+    xcd_block(bx, img);  // neighbouring bands share source rows: keep them in one L2
+    const int t = threadIdx.x;
+    const int dy0 = bx * kRsRows, nrow = min(kRsRows, L.h - dy0);
     const int ngrp = (L.w + 3) >> 2;
     int sstride;
     const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
@@ -349,8 +362,10 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     uint8_t* mm = (uint8_t*)(roi + RP * g.max_rh);             // u8 M, (max_wh + 2) x MP: px (x, y) at (y + 1) * MP + x + 2
     uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));      // pair queue: (y << 6) | x  (fd_pq entries)
     uint16_t* nq = pq + g.fd_pq;                               // NMS queue: (y << 6) | x  (max_win entries)
-    const int img = blockIdx.y, lane = threadIdx.x;
-    const int c_first = blockIdx.x * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
+    int bx, img;
+    xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
+    const int lane = threadIdx.x;
+    const int c_first = bx * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
     // ROI staging, 16 lanes per row (dword d), 4 rows per step (up to 16 steps = 64 rows): each slot is
     // one buffer_load_dwordx2 from the 4-byte aligned start of column -1, re-aligned with v_alignbyte.
     // The loads of the next cell are issued before this cell's compute (prefetch into registers).
@@ -1074,11 +1089,13 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
                                               const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur) {
     __shared__ __attribute__((aligned(16))) uint32_t src[kBlurWR * kBlurSD];
     __shared__ __attribute__((aligned(16))) uint32_t hor[(kBlurWR / 2) * kBlurTX];
-    const int img = blockIdx.y, t = threadIdx.x;
+    int bx, img;
+    xcd_block(bx, img);  // neighbouring tiles share 6 window rows / 8 columns: keep them in one L2
+    const int t = threadIdx.x;
     int l = 0;
-    while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].blur_tile0) ++l;
+    while (l + 1 < g.nlevels && bx >= g.lv[l + 1].blur_tile0) ++l;
     const LevelGeo& L = g.lv[l];
-    const int tile = blockIdx.x - L.blur_tile0;
+    const int tile = bx - L.blur_tile0;
     const int ntx = (L.w + kBlurTX - 1) / kBlurTX;
     const int ty = tile / ntx, tx = tile - ty * ntx;
     const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
