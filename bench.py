@@ -103,8 +103,8 @@ def main():
                     help="independent front-end handles per GPU, each on its own stream with P/streams pairs")
     ap.add_argument("--lanes", type=int, default=1, help="internal concurrent chunks per handle (orbfe_set_lanes)")
     ap.add_argument("--blur-fork", type=int, default=0,
-                    help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles
-                         already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
+                    help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles "
+                         "already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
     ap.add_argument("--cpu-sample", type=int, default=64, help="pairs timed for cpu_baseline (0 = skip; 64 is about 15 s)")
     ap.add_argument("--check", action="store_true", help="verify the last step's pair 0 against the oracle")
     ap.add_argument("--gather", action="store_true",
