@@ -62,3 +62,12 @@ def test_bad_params_fail_loudly():
         ORBextractor(2000, 1.2, 0, 20, 7)
     with pytest.raises(OrbfeError):
         ORBextractor(2000, 1.2, 8, 20, 7, resize_simd_lanes=8)
+
+
+def test_driver_scripts_compile():
+    """bench.py, __graft_entry__.py and the tools compile (the driver runs them on the GPU box)."""
+    import py_compile
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    for f in [root / "bench.py", root / "__graft_entry__.py", *sorted((root / "tools").glob("*.py"))]:
+        py_compile.compile(str(f), doraise=True, cfile="/dev/null")
