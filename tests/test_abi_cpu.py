@@ -66,8 +66,7 @@ def test_bad_params_fail_loudly():
 
 def test_driver_scripts_compile():
     """bench.py, __graft_entry__.py and the tools compile (the driver runs them on the GPU box)."""
-    import py_compile
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
     for f in [root / "bench.py", root / "__graft_entry__.py", *sorted((root / "tools").glob("*.py"))]:
-        py_compile.compile(str(f), doraise=True, cfile="/dev/null")
+        compile(f.read_text(), str(f), "exec")
