@@ -1507,9 +1507,11 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     __shared__ int sad[16][11];
     __shared__ uint8_t sL[16][121];
     __shared__ uint8_t sR[16][231];
-    const int pr = blockIdx.y, lane = threadIdx.x & 63, sl = lane & 15;
+    int bx, pr;
+    xcd_block(bx, pr);  // a pair's blocks read the same pyramids, descriptors and buckets: one L2
+    const int lane = threadIdx.x & 63, sl = lane & 15;
     const int kq = threadIdx.x >> 4;  // keypoint of this 16-lane group inside the block
-    const int iL = blockIdx.x * 16 + kq;
+    const int iL = bx * 16 + kq;
     const int nL = A.countL[pr * A.cnt_stride];
     const bool active = iL < nL;
     const orbfe_keypoint* KL = A.kpsL + pr * A.kp_stride;
