@@ -58,15 +58,15 @@ def algorithmic_bytes_per_pair(W, H, N=2000, nlevels=8):
     return total, per_stage
 
 
-def cpu_baseline(sample_pairs: int):
+def cpu_baseline(sample_pairs: int, width: int = 1241, height: int = 376, nfeatures: int = 2000):
     """Oracle extractor (C++ restatement, 1 thread) + numpy restatement of compute_stereo_matches on a
     bounded sample of the same synthetic workload, on this host."""
     from oracle.oracle import OracleExtractor
     from oracle import stereo_oracle
     from pyorbslam_amd import synth
-    exL, exR = OracleExtractor(), OracleExtractor()
+    exL, exR = OracleExtractor(nfeatures=nfeatures), OracleExtractor(nfeatures=nfeatures)
     t = exL.tables()
-    pairs = [synth.make_pair(10_000 + i) for i in range(sample_pairs)]
+    pairs = [synth.make_pair(10_000 + i, width, height) for i in range(sample_pairs)]
     t0 = time.perf_counter()
     for L, R in pairs:
         kl, dl = exL.extract(L)
@@ -75,7 +75,8 @@ def cpu_baseline(sample_pairs: int):
                                              t["scale"], t["inv_scale"], 386.1448, np.float32(718.856))
     dt = time.perf_counter() - t0
     return {"value": sample_pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_pairs} synthetic KITTI 1241x376 pairs (seeds 10000..), oracle C++ extractor "
+            "sample": f"{sample_pairs} synthetic {width}x{height} pairs, {nfeatures} features (seeds 10000..), "
+                      f"oracle C++ extractor "
                       f"(orb_oracle.cpp, -O2, 1 thread) + numpy compute_stereo_matches restatement, {dt:.1f} s"}
 
 
@@ -204,7 +205,8 @@ def main():
         chunk0 = (P // S) // max(1, min(args.lanes, P // S))
         dom = max(stage_ms, key=stage_ms.get) if stage_ms else "detect"
         ach = per_stage_b[dom] * chunk0 / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms else 0.0
-        workload = f"kitti{args.width}x{args.height}_synth_{args.nfeatures}f_{P}pairs"
+        cam = {(1241, 376): "kitti", (752, 480): "euroc"}.get((args.width, args.height), "custom")
+        workload = f"{cam}{args.width}x{args.height}_synth_{args.nfeatures}f_{P}pairs"
         tr = load_traffic(workload)
         out = {
             "metric": "stereo pairs/s (ORB extract L+R + stereo match), KITTI 1241x376, 1/2/4/8 GPU",
@@ -235,7 +237,7 @@ def main():
         if gather_s is not None:
             out["gather_s_untimed"] = round(gather_s, 4)
         if world == 1 and args.cpu_sample > 0:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.width, args.height, args.nfeatures)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
