@@ -65,6 +65,25 @@ __device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const u
     return ws + (int64_t)img * g.ws_bytes + g.lv[l].ws_off;
 }
 
+// A FAST cell's geometry as dword scalar loads (s_load) and SALU unpacking: reading the int16 fields
+// directly compiles to a per-lane global_load_ushort whose vmcnt wait also drains the next cell's ROI
+// prefetch — a full memory round trip per cell on the critical path.
+__device__ __forceinline__ CellGeo load_cell(const CellGeo* __restrict__ cells, int c) {
+    static_assert(sizeof(CellGeo) == 20, "CellGeo layout: 5 dwords");
+    const uint32_t* p = (const uint32_t*)(cells + c);
+    const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+    CellGeo cg;
+    cg.level = (int16_t)(w0 & 0xFFFFu);
+    cg.pad = (int16_t)(w0 >> 16);
+    cg.x0 = (int16_t)(w1 & 0xFFFFu);
+    cg.y0 = (int16_t)(w1 >> 16);
+    cg.x1 = (int16_t)(w2 & 0xFFFFu);
+    cg.y1 = (int16_t)(w2 >> 16);
+    cg.slot_off = (int)w3;
+    cg.slot_cap = (int)w4;
+    return cg;
+}
+
 // XCD-aware remap of a (gridDim.x, gridDim.y) grid.  Hardware block i (flattened, x fastest) runs on
 // XCD i % 8; the remap hands each XCD a contiguous run of logical blocks, so neighbouring tiles / cells /
 // bands — which share halo rows and partly used cache lines — meet in the same L2 instead of being
@@ -372,7 +391,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     const int d = lane & 15, r0 = lane >> 4;
     uint2 raw[16];
     auto issue = [&](int c) {
-        const CellGeo cg = cells[c];
+        const CellGeo cg = load_cell(cells, c);
         int stride;
         const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(lvl);
@@ -392,7 +411,7 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
     };
     if (c_first < c_last) issue(c_first);
     for (int c = c_first; c < c_last; ++c) {
-        const CellGeo cg = cells[c];
+        const CellGeo cg = load_cell(cells, c);
         const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
         const int ww = rw - 6, wh = rh - 6;  // detection window = ROI rows/cols 3 .. n-4
         {
@@ -655,8 +674,14 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
     uint16_t* kn_g = kn_all + (int64_t)img * g.key_total + L.key_off;
     uint32_t* out = lvl_kp + (int64_t)img * g.lvl_kp_cap + L.kp_off;
 
-    // 1. gather the level's candidates in cell order (= vToDistributeKeys order)
-    for (int i = t; i < ncell; i += kOctThreads) d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+    // 1. gather the level's candidates in cell order (= vToDistributeKeys order).  Each cell's slot
+    //    offset goes to LDS (cnt4 is free until pass 2) next to its count, so a key finds its slot with
+    //    LDS reads only and one global load
+    const bool soff_lds = ncell <= 4 * NC;
+    for (int i = t; i < ncell; i += kOctThreads) {
+        d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+        if (soff_lds) d.cnt4[i] = cells[L.cell0 + i].slot_off;
+    }
     __syncthreads();
     const int K = block_excl_scan(d.coff, ncell, scan_tmp);
     if (t == 0) d.coff[ncell] = K;
@@ -673,24 +698,47 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
             kn = kn_g;
         }
         const uint32_t* islots = slots + (int64_t)img * g.slot_total;
-        for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {  // 4 keys per step: their slot loads overlap
-            uint32_t v[4];
+        if (soff_lds) {
+            // key -> cell map in kn (rewritten by pass 2), one thread per cell
+            for (int i = t; i < ncell; i += kOctThreads)
+                for (int k = d.coff[i]; k < d.coff[i + 1]; ++k) kn[k] = (uint16_t)i;
+            __syncthreads();
+            for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {  // 4 keys per step: their slot loads overlap
+                uint32_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int k = k0 + u * kOctThreads;
-                v[u] = 0;
-                if (k < K) {
-                    int lo = 0, hi = ncell - 1;  // last cell with coff <= k
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u * kOctThreads;
+                    v[u] = 0;
+                    if (k < K) {
+                        const int c = kn[k];
+                        v[u] = islots[d.cnt4[c] + (k - d.coff[c])];
                     }
-                    v[u] = islots[cells[L.cell0 + lo].slot_off + (k - d.coff[lo])];
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (k0 + u * kOctThreads < K) kd[k0 + u * kOctThreads] = v[u];
+                for (int u = 0; u < 4; ++u)
+                    if (k0 + u * kOctThreads < K) kd[k0 + u * kOctThreads] = v[u];
+            }
+            __syncthreads();  // pass 2 clears cnt4 (the slot offsets) and rewrites kn
+        } else {
+            for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {
+                uint32_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u * kOctThreads;
+                    v[u] = 0;
+                    if (k < K) {
+                        int lo = 0, hi = ncell - 1;  // last cell with coff <= k
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+                        }
+                        v[u] = islots[cells[L.cell0 + lo].slot_off + (k - d.coff[lo])];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k0 + u * kOctThreads < K) kd[k0 + u * kOctThreads] = v[u];
+            }
         }
         mark(1);
         if (stop == 1) return;
