@@ -234,6 +234,13 @@ def main():
                          "pipeline_bytes_per_pair": total_b,
                          "pipeline_frac": round(pairs_per_s / world * total_b / (HBM_PEAK_GBS * 1e9), 6)},
         }
+        # the same roofline figures for every stage (handle 0's events, 64-pair launches)
+        out["stage_roofline"] = {
+            st: {"ms": round(stage_ms[st], 4),
+                 "achieved_GBs": round(per_stage_b[st] * chunk0 / (stage_ms[st] * 1e-3) / 1e9, 3),
+                 "frac": round(per_stage_b[st] * chunk0 / (stage_ms[st] * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                 "traffic": (tr or {}).get(st)}
+            for st in STAGES if stage_ms.get(st, 0) > 0}
         if gather_s is not None:
             out["gather_s_untimed"] = round(gather_s, 4)
         if world == 1 and args.cpu_sample > 0:
