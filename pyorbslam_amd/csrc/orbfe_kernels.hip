@@ -1569,9 +1569,11 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     const float2* rinfo = A.rinfo + pr * A.out_stride;
     if (sl < 11) sad[kq][sl] = 0;
     uint32_t key = 0xFFFFFFFFu;  // (distance << 16) | iR
-    orbfe_keypoint kl = {};
+    // the left record is read before the count is known (iL < kp_cap: inside the array), so the two
+    // loads overlap
+    orbfe_keypoint kl = KL[iL];
+    if (!active) kl = orbfe_keypoint{};
     if (active) {
-        kl = KL[iL];
         const int row = min((int)(double)kl.y, g.H - 1);
         const int* off = A.bucket_off + (int64_t)pr * (g.H + 1);
         const uint16_t* bidxs = A.bucket_idx + (int64_t)pr * A.bucket_cap;
@@ -1579,17 +1581,34 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         const float minU = __fsub_rn(kl.x, A.maxD);
         const uint4* dl4 = (const uint4*)(DL + (int64_t)iL * 32);
         const uint4 a0 = dl4[0], a1 = dl4[1];
-        for (int k = b + sl; k < e; k += 16) {
-            const int iR = bidxs[k];
-            const float2 ri = rinfo[iR];
-            const int oct = __float_as_int(ri.y);
-            if (oct < kl.octave - 1 || oct > kl.octave + 1) continue;
-            if (!(minU <= ri.x && (double)ri.x <= (double)kl.x)) continue;
-            const uint4* dr4 = (const uint4*)(DR + (int64_t)iR * 32);
-            const uint4 b0 = dr4[0], b1 = dr4[1];
-            const uint32_t dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-                                  __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-            key = min(key, (dist << 16) | (uint32_t)iR);
+        // kStU candidates per lane and step: all bucket reads, then all (x, octave) records and
+        // descriptors (read whether or not the gates pass) are in flight together — two dependent round
+        // trips per step instead of two per candidate
+        constexpr int kStU = 2;
+        for (int k0 = b + sl; k0 < e; k0 += 16 * kStU) {
+            int iR[kStU];
+#pragma unroll
+            for (int j = 0; j < kStU; ++j) iR[j] = k0 + 16 * j < e ? (int)bidxs[k0 + 16 * j] : -1;
+            float2 ri[kStU];
+            uint4 b0[kStU], b1[kStU];
+#pragma unroll
+            for (int j = 0; j < kStU; ++j) {
+                const int r = max(iR[j], 0);
+                ri[j] = rinfo[r];
+                const uint4* dr4 = (const uint4*)(DR + (int64_t)r * 32);
+                b0[j] = dr4[0];
+                b1[j] = dr4[1];
+            }
+#pragma unroll
+            for (int j = 0; j < kStU; ++j) {
+                const int oct = __float_as_int(ri[j].y);
+                const bool ok = iR[j] >= 0 && oct >= kl.octave - 1 && oct <= kl.octave + 1 && minU <= ri[j].x &&
+                                (double)ri[j].x <= (double)kl.x;
+                const uint32_t dist = __popc(a0.x ^ b0[j].x) + __popc(a0.y ^ b0[j].y) + __popc(a0.z ^ b0[j].z) +
+                                      __popc(a0.w ^ b0[j].w) + __popc(a1.x ^ b1[j].x) + __popc(a1.y ^ b1[j].y) +
+                                      __popc(a1.z ^ b1[j].z) + __popc(a1.w ^ b1[j].w);
+                if (ok) key = min(key, (dist << 16) | (uint32_t)iR[j]);
+            }
         }
     }
     key = row16_min(key);
