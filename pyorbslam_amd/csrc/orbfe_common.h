@@ -56,6 +56,8 @@ struct CellGeo {
 // Resize column entry.
 // k_blur output tile (the host counts tiles per level with the same numbers)
 constexpr int kBlurTX = 64, kBlurTY = 58;
+// k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
+constexpr int kOctKeys = 7424;
 
 struct ResizeX {
     int32_t sx;
@@ -80,6 +82,7 @@ struct Geo {
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count
     int max_ncap;        // octree node capacity (max over levels of kp_cap)
+    int oct_keys;        // octree candidates kept in LDS (kOctKeys, or 0 when the node arrays need the LDS)
     int rs_nsrc;         // k_resize: most source rows one 8-row output band needs
     int rs_sp;           // k_resize: largest source row stride (W for the input, pitch for derived levels)
     int rs_ngrp;         // k_resize: most 4-pixel groups in a derived level row (multiple of 4)

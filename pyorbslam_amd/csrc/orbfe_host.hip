@@ -356,6 +356,10 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.slot_total = std::max<int64_t>(slot_off, 1);
     g.key_total = std::max(key_off, 1);
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
+    // candidates in LDS when the node arrays leave room for them, else they stay in the global scratch
+    // (very large per-level feature counts, e.g. one level with thousands of features)
+    g.oct_keys = kOctKeys;
+    if (octree_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_keys = 0;
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024)
         throw Error(ORBFE_EINVAL, "octree LDS footprint exceeds the 160 KiB LDS of a CU (nfeatures per level too large)");
     c.W = W;

@@ -568,9 +568,8 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
 // LDS layout (dynamic, NC = Geo::max_ncap node slots):
 //   box[2][NC] u64 (x0,y0,x1,y1 int16) | cnt[2][NC] i32 | cnt4[4NC] i32 | cpos[4NC] u16 |
 //   sa[NC] sb[NC] sd[NC] proc[NC] i32 | srt[pow2(NC)] u64 | coff[maxcell+1] i32 |
-//   kd[kOctKeys] u32 | kn[kOctKeys] u16   (the candidates, when the level has at most kOctKeys; else they
+//   kd[g.oct_keys] u32 | kn[g.oct_keys] u16   (the candidates, when the level has at most g.oct_keys; else they
 //   stay in the global kd/kn arrays)
-constexpr int kOctKeys = 7424;     // with the node arrays: <= 80 KiB, two workgroups per CU
 constexpr int kOctThreads = 512;   // 8 waves: the per-pass candidate loops are latency chains
 struct OctLds {
     uint64_t *box0, *box1;
@@ -665,7 +664,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
         d.sd = (int*)p; p += 4 * NC;
         d.proc = (int*)p; p += 4 * NC;
         d.coff = (int*)p; p += 4 * ((maxcell + 4) & ~3);
-        d.kd = (uint32_t*)p; p += 4 * kOctKeys;
+        d.kd = (uint32_t*)p; p += 4 * g.oct_keys;
         d.kn = (uint16_t*)p;
     }
     const int N = L.n_feat;
@@ -1040,7 +1039,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
         if (t == 0) lvl_count[img * g.nlevels + l] = S;
         mark(63);
     };
-    if (K <= kOctKeys) run(std::true_type{});
+    if (K <= g.oct_keys) run(std::true_type{});
     else run(std::false_type{});
 }
 
@@ -1806,7 +1805,7 @@ size_t octree_lds_bytes(const Geo& g, int maxcell) {
     int pow2 = 1;
     while (pow2 < NC) pow2 <<= 1;
     return (size_t)8 * NC * 2 + 8 * pow2 + 4 * NC * 2 + 16 * NC + 8 * NC + 4 * NC * 4 + 4 * ((maxcell + 4) & ~3) +
-           6 * kOctKeys;
+           6 * (size_t)g.oct_keys;
 }
 
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,

@@ -139,3 +139,32 @@ def test_deterministic_repeat(cases):
     for _ in range(3):
         k2, d2 = ex.extract(img)
         assert k2.tobytes() == kps.tobytes() and np.array_equal(d2, desc)
+
+
+# extractor configurations other than the two cameras' (ORBextractor(nfeatures, scaleFactor, nlevels,
+# iniThFAST, minThFAST), ORBextractor.cpp:410-470): feature budgets, scale factors / level counts,
+# thresholds (including iniTh == minTh, where the fallback cannot change anything), other image sizes
+CONFIGS = [
+    ((376, 1241), dict(nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
+    ((376, 1241), dict(nfeatures=3000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=1.1, nlevels=12, iniThFAST=20, minThFAST=7)),
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=1.5, nlevels=5, iniThFAST=20, minThFAST=7)),
+    ((376, 1241), dict(nfeatures=1200, scaleFactor=1.3, nlevels=4, iniThFAST=12, minThFAST=5)),
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=1.2, nlevels=1, iniThFAST=20, minThFAST=7)),
+    ((376, 1241), dict(nfeatures=500, scaleFactor=1.2, nlevels=8, iniThFAST=30, minThFAST=15)),
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=9, minThFAST=9)),
+    ((720, 1280), dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
+    ((1080, 1920), dict(nfeatures=4000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(CONFIGS)))
+def test_extractor_configurations_bit_exact(ci):
+    (h, w), params = CONFIGS[ci]
+    img = synth.make_pair(200 + ci, w, h)[0]
+    kps, desc = ORBextractor(**params).extract(img)
+    okps, odesc = O.OracleExtractor(**params).extract(img)
+    assert len(kps) == len(okps) and len(kps) > 0
+    i, a, b = _first_diff(kps, okps)
+    assert i == len(kps), f"{params}: keypoint {i} differs: {a} vs {b}"
+    assert np.array_equal(desc, odesc), f"{params}: descriptors differ"
