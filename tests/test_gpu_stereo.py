@@ -120,3 +120,39 @@ def test_lanes_do_not_change_results(lanes):
     for p in range(5):
         a, b = ref.fetch_stereo(p), fe.fetch_stereo(p)
         assert all(np.array_equal(a[k], b[k]) for k in a)
+
+
+# other extractor configurations and baselines: GPU stereo against the numpy restatement (itself pinned to
+# the reference goldens above, tests/test_oracle_cpu.py), bit for bit
+STEREO_CONFIGS = [
+    ((376, 1241), dict(nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7), 386.1448, 718.856),
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=1.1, nlevels=12, iniThFAST=20, minThFAST=7), 386.1448, 718.856),
+    ((376, 1241), dict(nfeatures=1500, scaleFactor=1.5, nlevels=5, iniThFAST=15, minThFAST=5), 386.1448, 718.856),
+    ((480, 752), dict(nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7), 47.90639384423901,
+     435.2046959714599),
+    ((720, 1280), dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7), 250.0, 700.0),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(STEREO_CONFIGS)))
+def test_stereo_configurations_match_restatement(ci):
+    from oracle.oracle import OracleExtractor
+    (h, w), params, bf, fx = STEREO_CONFIGS[ci]
+    L, R = synth.make_pair(300 + ci, w, h)
+    exL, exR = ORBextractor(**params), ORBextractor(**params)
+    kl, dl = exL.extract(L)
+    kr, dr = exR.extract(R)
+    res = F.stereo_match_arrays(exL, exR, bf, np.float32(fx))
+    u, d = F.to_reference_lists(res, kl, bf)
+    oL, oR = OracleExtractor(**params), OracleExtractor(**params)
+    okl, odl = oL.extract(L)
+    okr, odr = oR.extract(R)
+    assert kl.tobytes() == okl.tobytes() and kr.tobytes() == okr.tobytes()
+    t = oL.tables()
+    ou, od, _ = stereo_oracle.compute_stereo_matches(okl, okr, odl, odr, oL.sheared_pyramid(), oR.sheared_pyramid(),
+                                                     t["scale"], t["inv_scale"], bf, np.float32(fx))
+    for a, b in ((u, ou), (d, od)):
+        sa, va = stereo_oracle.encode(a)
+        sb, vb = stereo_oracle.encode(b)
+        assert np.array_equal(sa, sb) and np.array_equal(va, vb)
+    assert int((res["status"] > 0).sum()) > 0
