@@ -1306,34 +1306,55 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
     const int img = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
     const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
     const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
-    const int wv = blk * kDescWaves + (threadIdx.x >> 6);
-    if (threadIdx.x < 256) s_pat[threadIdx.x] = ((const float4*)c_pattern)[threadIdx.x];
-    for (int i = threadIdx.x; i < 4 * 31 * 9; i += 64 * kDescWaves) (&s_mw[0][0])[i] = mw_tab[i];
-    // per level: keypoints (pre) and waves of 4 (wpre), wave-uniform
-    const int* cnt = lvl_count + img * g.nlevels;
-    int pre[kMaxLevels + 1], wpre[kMaxLevels + 1];
-    pre[0] = wpre[0] = 0;
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kDescWaves + (int)(threadIdx.x >> 6));  // wave-uniform
+    // the level tables are read into registers here and stored to LDS only after the pixel loads are
+    // issued: their round trip overlaps the keypoint's, and the barrier before the centroid covers them
+    constexpr int kMwPer = (4 * 31 * 9 + 64 * kDescWaves - 1) / (64 * kDescWaves);
+    float4 pat_r = {};
+    if (threadIdx.x < 256) pat_r = ((const float4*)c_pattern)[threadIdx.x];
+    uint2 mw_r[kMwPer];
 #pragma unroll
-    for (int i = 0; i < kMaxLevels; ++i) {
-        const int c = i < g.nlevels ? cnt[i] : 0;
-        pre[i + 1] = pre[i] + c;
-        wpre[i + 1] = wpre[i] + ((c + 3) >> 2);
+    for (int j = 0; j < kMwPer; ++j) {
+        const int i = threadIdx.x + j * 64 * kDescWaves;
+        mw_r[j] = i < 4 * 31 * 9 ? mw_tab[i] : uint2{0u, 0u};
     }
-    if (blk == 0 && threadIdx.x == 0) out_count[img] = pre[kMaxLevels];
-    __syncthreads();
-    if (wv >= wpre[kMaxLevels]) return;  // wave-uniform; no barrier follows
-    int l = 0;
+    // wave -> (level, 4-keypoint slot) from the level capacities (host constants), so the keypoint load
+    // does not wait for the octree's per-level counts: the counts, the keypoint and the level tables are
+    // one memory round trip, the pixels the next
+    int l = 0, w0 = 0;
+    {
+        bool go = true;
 #pragma unroll
-    for (int i = 1; i < kMaxLevels; ++i) l += (i < g.nlevels && wv >= wpre[i]) ? 1 : 0;
+        for (int i = 0; i + 1 < kMaxLevels; ++i) {
+            const int wc = (g.lv[i].kp_cap + 3) >> 2;
+            if (go && i + 1 < g.nlevels && wv >= w0 + wc) {
+                w0 += wc;
+                l = i + 1;
+            } else {
+                go = false;
+            }
+        }
+    }
     const LevelGeo& L = g.lv[l];
+    const int idx = 4 * (wv - w0) + q;  // keypoint of this row inside level l
+    const bool in_cap = idx < L.kp_cap;
+    const uint32_t key = in_cap ? lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx] : 0u;
+    const int* cnt = lvl_count + img * g.nlevels;
+    int pre[kMaxLevels + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxLevels; ++i) pre[i + 1] = pre[i] + (i < g.nlevels ? cnt[i] : 0);
+    if (blk == 0 && threadIdx.x == 0) out_count[img] = pre[kMaxLevels];
     const int n_l = pre[l + 1] - pre[l];
-    const int idx = 4 * (wv - wpre[l]) + q;  // keypoint of this row inside level l
-    const bool valid = idx < n_l;
+    const bool valid = in_cap && idx < n_l;
     const int o = pre[l] + idx;
-    const uint32_t key = valid ? lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx] : (20u | (20u << 12));
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    const int cx = key & 0xFFF, cy = (key >> 12) & 0xFFF, score = key >> 24;
+    // slots past the level's count hold stale keys: clamp them to where real keypoints lie
+    // ([19, w - 20] x [19, h - 20]) so every row's loads stay inside the level
+    const int cx = min(max((int)(key & 0xFFF), kEdge), L.w - kEdge - 1);
+    const int cy = min(max((int)((key >> 12) & 0xFFF), kEdge), L.h - kEdge - 1);
+    const int score = key >> 24;
     // ---- intensity centroid: 18 dwords per lane, buffer loads at 32-bit offsets from the level base
     const uint32_t off0 = (uint32_t)((cy - kHalfPatch) * stride + cx - kHalfPatch);
     const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
@@ -1382,6 +1403,13 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
             }
         }
     }
+    if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
+#pragma unroll
+    for (int j = 0; j < kMwPer; ++j) {
+        const int i = threadIdx.x + j * 64 * kDescWaves;
+        if (i < 4 * 31 * 9) (&s_mw[0][0])[i] = mw_r[j];
+    }
+    __syncthreads();  // the level tables (s_mw, s_pat) are in LDS
     // m10 = sum (u0 + b) val_b, m01 = sum v val_b with non-negative byte weights (u0 + 18 + b), (v + 15)
     // accumulated by v_dot4 and corrected by -18 / -15 x sum(val); masks and m10 weights from s_mw
     uint32_t a10 = 0, a01 = 0, a1 = 0;
