@@ -677,9 +677,11 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
     //    offset goes to LDS (cnt4 is free until pass 2) next to its count, so a key finds its slot with
     //    LDS reads only and one global load
     const bool soff_lds = ncell <= 4 * NC;
-    for (int i = t; i < ncell; i += kOctThreads) {
-        d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
-        if (soff_lds) d.cnt4[i] = cells[L.cell0 + i].slot_off;
+    for (int i = t; i < ncell; i += kOctThreads) {  // both loads in flight before either store
+        const int n = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+        const int so = soff_lds ? cells[L.cell0 + i].slot_off : 0;
+        d.coff[i] = n;
+        if (soff_lds) d.cnt4[i] = so;
     }
     __syncthreads();
     const int K = block_excl_scan(d.coff, ncell, scan_tmp);
