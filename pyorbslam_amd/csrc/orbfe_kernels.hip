@@ -1566,6 +1566,27 @@ __device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int 
     const int pw = w + 2 * kEdge;
     const int f = kEdge * pw + kEdge + r * w + c0;
     int pr = f / pw, pc = f - pr * pw;
+    if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
+        // the run lies inside one row of the level (the common case): 6 dword loads from the aligned
+        // start, bounded to the level (reads past its end return 0), bytes re-aligned with v_alignbyte
+        const uint64_t a64 = (uint64_t)(uintptr_t)lvl;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)a64, 0, (uint32_t)(stride * h), 0x00020000);
+        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge));
+        const uint32_t sh = (uint32_t)((a64 + off) & 3u), al = off - sh;
+        uint32_t d[7];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * k, 0, 0);
+        d[6] = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t wd = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (4 * k + b < n) dst[4 * k + b] = (uint8_t)(wd >> (8 * b));
+        }
+        return;
+    }
     uint8_t v[21];
 #pragma unroll
     for (int j = 0; j < 21; ++j) {
