@@ -991,10 +991,11 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
-                    // variant 0 blur + describe, 1 blur, 2 describe, 4 describe with 4-wave workgroups
-                    if (variant <= 1)
-                        HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s));
-                    if (variant != 1)
+                    // variant 0 blur + describe, 1 blur, 2 describe, 4 describe with 4-wave workgroups,
+                    // 5 blur without its stores (probe)
+                    if (variant <= 1 || variant == 5)
+                        HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s, variant == 5));
+                    if (variant != 1 && variant != 5)
                         HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
                                               h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_mw.p,
                                               n, s, variant == 4 ? 4 : 0));

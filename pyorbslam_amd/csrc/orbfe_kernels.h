@@ -50,7 +50,7 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
                          hipStream_t s, int variant = 0, long long* prof = nullptr);
 hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* blur, int n_images,
-                       hipStream_t s);
+                       hipStream_t s, int probe = 0);
 hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
                            const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
                            int* out_count, const uint32_t* mw, int n_images, hipStream_t s, int variant = 0);

@@ -1125,7 +1125,12 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 //    holds (H[2m][x], H[2m+1][x]).
 //  * vertical: output rows 2n+3 and 2n+4 of the window from the 4 interleaved dwords P(n) .. P(n+3),
 //    4 x v_dot2_u32_u16 each with the +2^15 rounding as the accumulator seed; 2 aligned dword stores.
-constexpr int kBlurWR = kBlurTY + 6;        // staged window rows (64)
+constexpr int kBlurWR = kBlurTY + 6;        // staged window rows
+static_assert((kBlurWR / 2) * (kBlurTX / 4) % 256 == 0, "horizontal items: a whole number per thread");
+// slot / 18 as a 24-bit multiply and shift, exact for every staging slot of the window
+constexpr uint32_t kBlurDiv18Sh = kBlurWR * 18 <= 1152 ? 16 : 17;
+constexpr uint32_t kBlurDiv18 = kBlurDiv18Sh == 16 ? 3641u : 7282u;
+static_assert(kBlurWR * 18 <= 2304, "staging slot division range");
 constexpr int kBlurWD = (kBlurTX + 8) / 4;  // staged dwords per row (18)
 constexpr int kBlurSD = 20;                 // LDS pitch of a staged row, dwords
 
@@ -1135,7 +1140,7 @@ __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clam
 }
 
 __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
-                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur) {
+                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur, int probe) {
     __shared__ __attribute__((aligned(16))) uint32_t src[kBlurWR * kBlurSD];
     __shared__ __attribute__((aligned(16))) uint32_t hor[(kBlurWR / 2) * kBlurTX];
     int bx, img;
@@ -1169,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             const uint32_t slot = (uint32_t)(t + 256 * k);
-            const uint32_t r = __umul24(slot, 3641u) >> 16, d = slot - 18u * r;
+            const uint32_t r = __umul24(slot, kBlurDiv18) >> kBlurDiv18Sh, d = slot - 18u * r;
             const int x = X0 - 4 + 4 * (int)d;  // image column of the dword's first byte
             raw[k] = uint2{0u, 0u};
             sh[k] = 0;
@@ -1191,10 +1196,13 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     if (left || right) {  // patch the reflected columns (sources lie inside the window, never patched)
         __syncthreads();
         uint8_t* sb = (uint8_t*)src;
-        uint8_t v[2] = {0, 0};
-        int o[2] = {-1, -1};
+        constexpr int NP = (kBlurWR * 6 + 255) / 256;
+        uint8_t v[NP];
+        int o[NP];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < NP; ++k) {
+            v[k] = 0;
+            o[k] = -1;
             const int i = t + 256 * k;
             const int r = i / 6, j = i - r * 6;
             const int x = j < 3 ? j - 3 : L.w + j - 3;  // -3 .. -1, w .. w+2
@@ -1206,7 +1214,7 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < NP; ++k)
             if (o[k] >= 0) sb[o[k]] = v[k];
     }
     __syncthreads();
@@ -1258,6 +1266,10 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
             o |= (b >> 16) << (8 * c);
         }
         // rows are padded to a 16-byte pitch, so the dwords never leave the row's allocation
+        if (probe == 1) {  // microbench probe: no stores unless the value is impossible
+            if (e == 0x12345678u && o == 0x9abcdef0u) *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = e;
+            continue;
+        }
         *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = e;
         if (y + 1 < L.h) *(uint32_t*)(dstimg + (int64_t)(y + 1) * L.pitch + x) = o;
     }
@@ -1873,8 +1885,8 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
 }
 
 hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* blur, int n_images,
-                       hipStream_t s) {
-    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur);
+                       hipStream_t s, int probe) {
+    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur, probe);
     return hipGetLastError();
 }
 
