@@ -371,7 +371,7 @@ __device__ __forceinline__ int lanes_below(uint64_t b) {
 // V: 0 full kernel; ablations for tools/microbench.py: 1 ROI staging only, 2 + pre-test, 3 + M.
 // RP: ROI pitch in u16 (48, 64 or 96; >= widest ROI + 3).
 template <int V, int RP>
-__global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64, 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
     constexpr int S = RP / 2;
@@ -454,28 +454,43 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
         const int step_y = 64 / qrow, step_x = 64 - step_y * qrow;
         int npq = 0;
         {
+            // two 64-quad steps per iteration: both steps' ROI reads are issued before either waits
+            // (one LDS round trip per 128 quads); lanes past the window read a clamped row and vote 0
             int qy = lane / qrow, qx = lane - (lane / qrow) * qrow;
-            for (int i0 = 0; i0 < nquad; i0 += 64) {
-                const int x = 4 * qx;
-                bool ca = false, cb = false;
-                if (i0 + lane < nquad) {
-                    fd_s2 ba, bb;
-                    fast_bound_quad<S>((const uint32_t*)(roi + ((qy & 63) + 3) * RP + x + 4), ba, bb);
-                    ca = ba.x > tq || (ba.y > tq && x + 1 < ww);
-                    cb = x + 2 < ww && (bb.x > tq || (bb.y > tq && x + 3 < ww));
+            auto advance = [&](int& y, int& x) {
+                y += step_y;
+                x += step_x;
+                if (x >= qrow) {
+                    x -= qrow;
+                    ++y;
                 }
+            };
+            auto bound = [&](int i, int y, int x4, bool& ca, bool& cb) {
+                fd_s2 ba, bb;
+                fast_bound_quad<S>((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4), ba, bb);
+                const bool in = i < nquad;
+                ca = in & ((ba.x > tq) | ((ba.y > tq) & (x4 + 1 < ww)));
+                cb = in & (x4 + 2 < ww) & ((bb.x > tq) | ((bb.y > tq) & (x4 + 3 < ww)));
+            };
+            auto emit = [&](int y, int x4, bool ca, bool cb) {
                 const uint64_t b0 = __ballot(ca), b1 = __ballot(cb);
                 const int o = npq + lanes_below(b0) + lanes_below(b1);
-                const uint16_t e = (uint16_t)((qy << 6) | x);
+                const uint16_t e = (uint16_t)((y << 6) | x4);
                 if (ca) pq[o] = e;
                 if (cb) pq[o + (int)ca] = (uint16_t)(e + 2);
                 npq += __popcll(b0) + __popcll(b1);
-                qy += step_y;
-                qx += step_x;
-                if (qx >= qrow) {
-                    qx -= qrow;
-                    ++qy;
-                }
+            };
+            for (int i0 = 0; i0 < nquad; i0 += 128) {
+                int qy2 = qy, qx2 = qx;
+                advance(qy2, qx2);
+                bool ca0, cb0, ca1, cb1;
+                bound(i0 + lane, qy, 4 * qx, ca0, cb0);
+                bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1);
+                emit(qy, 4 * qx, ca0, cb0);
+                emit(qy2, 4 * qx2, ca1, cb1);
+                qy = qy2;
+                qx = qx2;
+                advance(qy, qx);
             }
         }
         __syncthreads();
@@ -486,11 +501,13 @@ __global__ __launch_bounds__(64) void k_detect(Geo g, const CellGeo* __restrict_
         // ---- 3. exact M of the queued pairs -> M map; NMS candidates -> queue
         const int tlow = max(tq, 1);
         int nnq = 0;
+        // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
+        uint32_t e_next = lane < npq ? pq[lane] : 0u;
         for (int k0 = 0; k0 < npq; k0 += 64) {
             bool h0 = false, h1 = false;
-            uint32_t e = 0;
+            const uint32_t e = e_next;
+            if (k0 + 64 + lane < npq) e_next = pq[k0 + 64 + lane];
             if (k0 + lane < npq) {
-                e = pq[k0 + lane];
                 const int x = e & 63, y = e >> 6;
                 uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
                 if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
