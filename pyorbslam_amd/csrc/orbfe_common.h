@@ -91,7 +91,8 @@ struct Geo {
     int max_wh;          // largest FAST detection window height (rows)
     int max_win;         // largest FAST detection window (pixels), rounded up to 16
     int fd_mp;           // k_detect: u8 M map pitch in bytes (>= widest window + 6, multiple of 16)
-    int fd_pq;           // k_detect: pair-queue entries (>= ceil(ww/2) * wh and >= 2 * slot_cap)
+    int fd_pq;           // k_detect: pair-queue entries (>= ceil(ww/2) * wh)
+    int fd_alt;          // k_detect: largest cell slot_cap (minTh survivors staged in the ROI area)
     int umax[16];
     float scale[kMaxLevels];
     float inv_scale[kMaxLevels];

@@ -293,8 +293,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     cg.x1 = (int16_t)(int)maxXc;
                     cg.y1 = (int16_t)(int)maxYc;
                     const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0;
-                    // k_detect stages a ROI row from column -1 as 16 re-aligned dwords (<= 63 px)
-                    if (rw > 63 || rh > 64) throw Error(ORBFE_EINVAL, "FAST cell ROI larger than 63 x 64 px");
+                    // k_detect stages a ROI row from column -1 as <= 16 dwords, one per lane of a 16-lane DPP row
+                    if (rw > 59 || rh > 64) throw Error(ORBFE_EINVAL, "FAST cell ROI larger than 59 x 64 px");
                     if (cg.x0 < 1) throw Error(ORBFE_EINVAL, "FAST cell ROI at column 0");
                     const int ww = std::max(rw - 6, 0), wh = std::max(rh - 6, 0);
                     g.max_rh = std::max(g.max_rh, rh);
@@ -304,8 +304,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     g.fd_mp = std::max(g.fd_mp, (ww + 6 + 15) & ~15);
                     cg.slot_off = (int)slot_off;
                     cg.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
-                    // k_detect's pair queue also stages the minTh survivors (u32 = 2 entries each)
-                    g.fd_pq = std::max(g.fd_pq, (std::max(((ww + 1) / 2) * wh, 2 * cg.slot_cap) + 7) & ~7);
+                    g.fd_pq = std::max(g.fd_pq, (((ww + 1) / 2) * wh + 7) & ~7);
+                    g.fd_alt = std::max(g.fd_alt, cg.slot_cap);
                     slot_off += cg.slot_cap;
                     key_cap += cg.slot_cap;
                     c.cells.push_back(cg);

@@ -368,28 +368,39 @@ __device__ __forceinline__ int lanes_below(uint64_t b) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
 }
 
+// u16 elements of k_detect's ROI area: the ROI itself, and after the M stage the minTh survivors of a cell
+// (u32 records, at most slot_cap = Geo::fd_alt); a multiple of 8 so the M map after it is 16-byte aligned
+__host__ __device__ inline int detect_roi_elems(const Geo& g, int rp) {
+    const int n = rp * g.max_rh > 2 * g.fd_alt ? rp * g.max_rh : 2 * g.fd_alt;
+    return (n + 7) & ~7;
+}
+
 // V: 0 full kernel; ablations for tools/microbench.py: 1 ROI staging only, 2 + pre-test, 3 + M.
-// RP: ROI pitch in u16 (48, 64 or 96; >= widest ROI + 3).
-template <int V, int RP>
-__global__ __launch_bounds__(64, 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
+// RP: ROI pitch in u16 (48, 64 or 96; >= widest ROI + 3).  NS: staged row slots (4 rows each, >= max_rh / 4).
+// 5 waves per SIMD (<= 96 VGPRs) and <= 8 KiB of LDS for KITTI / EuRoC cells: detect is bound by how many
+// cells are in flight per CU (16 -> 10 resident waves costs +32 %, tools/microbench.py variant 8).
+template <int V, int RP, int NS>
+__global__ __launch_bounds__(64, 5) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
     constexpr int S = RP / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint16_t* roi = (uint16_t*)lds;                            // max_rh rows x RP
+    // ROI (max_rh rows x RP u16); after the M stage the same bytes stage the minTh survivors (u32 records)
+    uint16_t* roi = (uint16_t*)lds;
     const int MP = g.fd_mp & 0xFFFF;  // provably 16-bit: row offsets use v_mul_u32_u24
-    uint8_t* mm = (uint8_t*)(roi + RP * g.max_rh);             // u8 M, (max_wh + 2) x MP: px (x, y) at (y + 1) * MP + x + 2
-    uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));      // pair queue: (y << 6) | x  (fd_pq entries)
-    uint16_t* nq = pq + g.fd_pq;                               // NMS queue: (y << 6) | x  (max_win entries)
+    uint8_t* mm = (uint8_t*)(roi + detect_roi_elems(g, RP));   // u8 M, (max_wh + 2) x MP: px (x, y) at (y + 1) * MP + x + 2
+    // pair queue (y << 6) | x, x even (fd_pq entries); the M stage compacts it in place into the NMS queue
+    uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));
     int bx, img;
     xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
     const int lane = threadIdx.x;
     const int c_first = bx * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
-    // ROI staging, 16 lanes per row (dword d), 4 rows per step (up to 16 steps = 64 rows): each slot is
-    // one buffer_load_dwordx2 from the 4-byte aligned start of column -1, re-aligned with v_alignbyte.
-    // The loads of the next cell are issued before this cell's compute (prefetch into registers).
+    // ROI staging, 16 lanes per row (dword d), 4 rows per step (NS steps): lane d loads dword d of the row
+    // from the 4-byte aligned start of column -1 and takes dword d + 1 from its neighbour lane (DPP
+    // row_shl:1) to re-align with v_alignbyte (rows are <= 59 px, so 16 dwords cover every row).  The
+    // loads of the next cell are issued before this cell's compute (prefetch into NS registers).
     const int d = lane & 15, r0 = lane >> 4;
-    uint2 raw[16];
+    uint32_t raw[NS];
     auto issue = [&](int c) {
         const CellGeo cg = load_cell(cells, c);
         int stride;
@@ -399,13 +410,13 @@ __global__ __launch_bounds__(64, 4) void k_detect(Geo g, const CellGeo* __restri
         const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
         const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < NS; ++k) {
             const int r = r0 + 4 * k;
-            raw[k] = uint2{0u, 0u};
-            if (r < rh && d < ndw) {
+            raw[k] = 0u;
+            if (r < rh && d <= ndw) {
                 const uint32_t off = off0 + (uint32_t)(4 * k * stride);
                 const uint32_t al = off - ((lvl_lo + off) & 3u);
-                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al + 4u * d, 0, 0));
+                raw[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * d, 0, 0);
             }
         }
     };
@@ -421,11 +432,13 @@ __global__ __launch_bounds__(64, 4) void k_detect(Geo g, const CellGeo* __restri
             const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
             const int ndw = (rw + 4) >> 2;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+            for (int k = 0; k < NS; ++k) {
+                // every lane takes part in the DPP (uniform control flow); lanes 15 of a row get 0
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)raw[k], 0x101, 0xF, 0xF, false);
                 const int r = r0 + 4 * k;
                 if (r < rh && d < ndw) {
                     const int sh = (int)((lvl_lo + off0 + (uint32_t)(4 * k * stride)) & 3u);
-                    const uint32_t w = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh);
+                    const uint32_t w = __builtin_amdgcn_alignbyte(nb, raw[k], sh);
                     uint2 u;
                     u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04010400u);
                     u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04030402u);
@@ -516,50 +529,60 @@ __global__ __launch_bounds__(64, 4) void k_detect(Geo g, const CellGeo* __restri
                 h0 = (int)(m & 0x3FFu) > tlow;
                 h1 = (int)((m >> 16) & 0x3FFu) > tlow;
             }
-            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-            const int o = nnq + lanes_below(b0) + lanes_below(b1);
-            if (h0) nq[o] = (uint16_t)e;
-            if (h1) nq[o + (int)h0] = (uint16_t)(e + 1);
-            nnq += __popcll(b0) + __popcll(b1);
+            // pairs with a pixel above tlow are compacted in place: slots < k0 + 64 are written, every read of
+            // the queue (this step's entries, the next step's prefetch) was issued before
+            const bool h = h0 | h1;
+            const uint64_t bh = __ballot(h);
+            if (h) pq[nnq + lanes_below(bh)] = (uint16_t)e;
+            nnq += __popcll(bh);
         }
         __syncthreads();
         if (V == 3) {  // ablation: + exact M
             if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
             return;
         }
-        // ---- 4. NMS (local max) over the queue + ordered compaction, both thresholds in one pass: the
-        //         neighbour maximum does not depend on t, so each entry is tested at iniTh and minTh
-        //         together.  iniTh survivors go straight out; minTh survivors are staged in the (free) pixel
-        //         queue area and copied out only if iniTh kept nothing (ORBextractor.cpp:811-815).
+        // ---- 4. NMS (local max) over the queued pairs + ordered compaction, both thresholds in one pass:
+        //         the neighbour maximum does not depend on t, so each pixel is tested at iniTh and minTh
+        //         together (own > max(neighbours, th) also implies own > tlow).  iniTh survivors go straight
+        //         out; minTh survivors are staged in the (dead) ROI area and copied out only if iniTh kept
+        //         nothing (ORBextractor.cpp:811-815).  Output order: pairs row-major, pixel x before x + 1.
         uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
-        uint32_t* alt = (uint32_t*)pq;  // 2 * slot_cap <= fd_pq entries (host)
+        uint32_t* alt = (uint32_t*)roi;  // >= 2 * slot_cap u16 (detect_roi_elems)
         const bool fb = g.min_th != g.ini_th;
         const int thb0 = max(g.ini_th, 1), thb1 = max(g.min_th, 1);
         int t0 = 0, t1 = 0;
         for (int k0 = 0; k0 < nnq; k0 += 64) {
-            bool keep0 = false, keep1 = false;
-            uint32_t rec = 0;
+            bool ka0 = false, kb0 = false, ka1 = false, kb1 = false;
+            uint32_t reca = 0, recb = 0;
             if (k0 + lane < nnq) {
-                const int e = nq[k0 + lane];
-                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;
-                const int own = q[0];
-                const int nmax = max(imax3(q[-MP - 1], q[-MP], q[-MP + 1]),
-                                     imax3(q[MP - 1], q[MP], max(q[MP + 1], max(q[-1], q[1]))));
-                keep0 = own > max(nmax, thb0);
-                keep1 = own > max(nmax, thb1);
-                rec = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12) |
-                      ((uint32_t)(own - 1) << 24);
+                const int e = pq[k0 + lane];
+                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
+                const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
+                const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
+                const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
+                const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
+                const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
+                const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
+                ka0 = owna > max(na, thb0);
+                ka1 = owna > max(na, thb1);
+                kb0 = ownb > max(nb, thb0);
+                kb1 = ownb > max(nb, thb1);
+                const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
+                reca = xy | ((uint32_t)(owna - 1) << 24);
+                recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
             }
-            const uint64_t bal0 = __ballot(keep0);
-            const int o0 = t0 + lanes_below(bal0);
+            const uint64_t ba0 = __ballot(ka0), bb0 = __ballot(kb0);
+            const int o0 = t0 + lanes_below(ba0) + lanes_below(bb0);
             // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-            if (keep0 && o0 < cg.slot_cap) out[o0] = rec;
-            t0 += __popcll(bal0);
+            if (ka0 && o0 < cg.slot_cap) out[o0] = reca;
+            if (kb0 && o0 + (int)ka0 < cg.slot_cap) out[o0 + (int)ka0] = recb;
+            t0 += __popcll(ba0) + __popcll(bb0);
             if (fb) {
-                const uint64_t bal1 = __ballot(keep1);
-                const int o1 = t1 + lanes_below(bal1);
-                if (keep1 && o1 < cg.slot_cap) alt[o1] = rec;
-                t1 += __popcll(bal1);
+                const uint64_t ba1 = __ballot(ka1), bb1 = __ballot(kb1);
+                const int o1 = t1 + lanes_below(ba1) + lanes_below(bb1);
+                if (ka1 && o1 < cg.slot_cap) alt[o1] = reca;
+                if (kb1 && o1 + (int)ka1 < cg.slot_cap) alt[o1 + (int)ka1] = recb;
+                t1 += __popcll(ba1) + __popcll(bb1);
             }
         }
         int total = t0;
@@ -1854,28 +1877,35 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 int detect_rp(const Geo& g) { return g.max_rw + 3 <= 48 ? 48 : g.max_rw + 3 <= 64 ? 64 : 96; }
 
 size_t detect_lds_bytes(const Geo& g) {
-    return 2 * (size_t)detect_rp(g) * g.max_rh + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.fd_pq +
-           2 * (size_t)g.max_win;
+    return 2 * (size_t)detect_roi_elems(g, detect_rp(g)) + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.fd_pq;
 }
 
-template <int RP>
+template <int RP, int NS>
 static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                              int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
     // variants 8 / 9: the full kernel with 6 / 12 KiB of extra (unused) LDS, to measure how detect
     // time depends on occupancy (tools/microbench.py)
     const size_t lds = detect_lds_bytes(g) + (variant == 8 ? 6144 : variant == 9 ? 12288 : 0);
     const dim3 grid((g.ncells + kFdCells - 1) / kFdCells, n_images), blk(64);
-    auto k = variant == 1 ? k_detect<1, RP> : variant == 2 ? k_detect<2, RP> : variant == 3 ? k_detect<3, RP>
-                                                                                           : k_detect<0, RP>;
+    auto k = variant == 1 ? k_detect<1, RP, NS> : variant == 2 ? k_detect<2, RP, NS> : variant == 3 ? k_detect<3, RP, NS>
+                                                                                           : k_detect<0, RP, NS>;
     hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
 }
 
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
+    // ROIs of at most 48 rows (KITTI, EuRoC) stage from 12 registers, taller ones (<= 64) from 16
+    const bool tall = g.max_rh > 48;
     switch (detect_rp(g)) {
-        case 48: launch_detect_rp<48>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant); break;
-        case 64: launch_detect_rp<64>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant); break;
-        default: launch_detect_rp<96>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+        case 48:
+            if (tall) launch_detect_rp<48, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            else launch_detect_rp<48, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            break;
+        case 64:
+            if (tall) launch_detect_rp<64, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            else launch_detect_rp<64, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            break;
+        default: launch_detect_rp<96, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
     }
     return hipGetLastError();
 }
