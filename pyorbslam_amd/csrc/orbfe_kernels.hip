@@ -377,10 +377,11 @@ __host__ __device__ inline int detect_roi_elems(const Geo& g, int rp) {
 
 // V: 0 full kernel; ablations for tools/microbench.py: 1 ROI staging only, 2 + pre-test, 3 + M.
 // RP: ROI pitch in u16 (48, 64 or 96; >= widest ROI + 3).  NS: staged row slots (4 rows each, >= max_rh / 4).
-// 5 waves per SIMD (<= 96 VGPRs) and <= 8 KiB of LDS for KITTI / EuRoC cells: detect is bound by how many
+// 5 waves per SIMD (<= 96 VGPRs; 4 for the wider / taller ROI variants, which need the registers) and
+// <= 8 KiB of LDS for KITTI / EuRoC cells: detect is bound by how many
 // cells are in flight per CU (16 -> 10 resident waves costs +32 %, tools/microbench.py variant 8).
 template <int V, int RP, int NS>
-__global__ __launch_bounds__(64, 5) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
     constexpr int S = RP / 2;
