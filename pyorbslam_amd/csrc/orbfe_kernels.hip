@@ -1088,24 +1088,24 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
 
 // ------------------------------------------------------------------------------- descriptor math
 // glibc 2.35 x86-64 sinf / cosf (FMA ifunc variant; ARM optimized-routines algorithm), |x| < 120.
-struct SinCosTab {
-    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
-__constant__ SinCosTab c_sc[2] = {
-    {{1, -1, -1, 1}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p+0, -0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
-    {{1, -1, -1, 1}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p+0, 0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
+// glibc's two coefficient tables differ only in the sign of the cosine coefficients, so the second
+// table's cosine polynomial is the negated first one (fma(a, -b, -c) == -fma(a, b, c), exactly), and the
+// quadrant sign {1, -1, -1, 1}[n & 3] is a negation when bit 0 ^ bit 1 of n is set.  Everything is an
+// immediate: a lane-indexed __constant__ table compiles to two dependent vector memory round trips.
+namespace sc {
+constexpr double hpi_inv = 0x1.45f306dc9c883p+23, hpi = 0x1.921fb54442d18p+0;
+constexpr double c0 = 0x1p+0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                 c4 = 0x1.99343027bf8c3p-16;
+constexpr double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+}  // namespace sc
 
-__device__ __forceinline__ float sc_sin_poly(double x, double x2, const SinCosTab& p) {
-    const double x3 = x * x2, s1 = __fma_rn(x2, p.s3, p.s2), x5 = x2 * x3, s = __fma_rn(x3, p.s1, x);
+__device__ __forceinline__ float sc_sin_poly(double x, double x2) {
+    const double x3 = x * x2, s1 = __fma_rn(x2, sc::s3, sc::s2), x5 = x2 * x3, s = __fma_rn(x3, sc::s1, x);
     return (float)__fma_rn(x5, s1, s);
 }
-__device__ __forceinline__ float sc_cos_poly(double x2, const SinCosTab& p) {
-    const double x4 = x2 * x2, c1 = __fma_rn(x2, p.c1, p.c0), c2 = __fma_rn(x2, p.c4, p.c3), x6 = x2 * x4;
-    const double c = __fma_rn(x4, p.c2, c1);
+__device__ __forceinline__ float sc_cos_poly(double x2) {
+    const double x4 = x2 * x2, c1 = __fma_rn(x2, sc::c1, sc::c0), c2 = __fma_rn(x2, sc::c4, sc::c3), x6 = x2 * x4;
+    const double c = __fma_rn(x4, sc::c2, c1);
     return (float)__fma_rn(x6, c2, c);
 }
 __device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
@@ -1113,23 +1113,19 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
     double x = y;
     if (top <= 0x3f3) {
         const double x2 = x * x;
-        *sn = top <= 0x397 ? y : sc_sin_poly(x, x2, c_sc[0]);
-        *cs = top <= 0x397 ? 1.0f : sc_cos_poly(x2, c_sc[0]);
+        *sn = top <= 0x397 ? y : sc_sin_poly(x, x2);
+        *cs = top <= 0x397 ? 1.0f : sc_cos_poly(x2);
         return;
     }
-    const double r = x * c_sc[0].hpi_inv;
+    const double r = x * sc::hpi_inv;
     const int n = (((int)r) + 0x800000) >> 24;
-    x = __fma_rn(-(double)n, c_sc[0].hpi, x);
-    const SinCosTab& p = c_sc[(n >> 1) & 1];
+    x = __fma_rn(-(double)n, sc::hpi, x);
     const double x2 = x * x;
-    const double xs = x * c_sc[0].sign[n & 3];
-    if (n & 1) {
-        *sn = sc_cos_poly(x2, p);
-        *cs = sc_sin_poly(xs, x2, p);
-    } else {
-        *sn = sc_sin_poly(xs, x2, p);
-        *cs = sc_cos_poly(x2, p);
-    }
+    const double xs = ((n ^ (n >> 1)) & 1) ? -x : x;
+    const float cp = ((n >> 1) & 1) ? -sc_cos_poly(x2) : sc_cos_poly(x2);
+    const float sp = sc_sin_poly(xs, x2);
+    *sn = (n & 1) ? cp : sp;
+    *cs = (n & 1) ? sp : cp;
 }
 
 // cv::fastAtan2, plain IEEE float ops (no contraction)
