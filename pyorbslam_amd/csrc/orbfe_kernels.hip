@@ -1566,12 +1566,15 @@ __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
     int* off = A.bucket_off + (int64_t)pr * (H + 1);
     uint16_t* idx = A.bucket_idx + (int64_t)pr * A.bucket_cap;
     float2* rinfo = A.rinfo + pr * A.out_stride;
+    // per-octave scales in LDS: a lane-indexed read of the kernel argument would be a vector memory load
+    __shared__ float s_scale[kMaxLevels];
+    if (t < kMaxLevels) s_scale[t] = g.scale[t];
     for (int i = t; i <= H; i += 256) cnt[i] = 0;
     __syncthreads();
     for (int i = t; i < nR; i += 256) {
         const orbfe_keypoint kr = KR[i];
         rinfo[i] = make_float2(kr.x, __int_as_float(kr.octave));
-        const double r = 2.0 * (double)g.scale[kr.octave];
+        const double r = 2.0 * (double)s_scale[kr.octave];
         const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
         for (int y = lo; y <= hi; ++y) atomicAdd(&cnt[y], 1);
     }
@@ -1583,7 +1586,7 @@ __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
     __syncthreads();
     for (int i = t; i < nR; i += 256) {
         const orbfe_keypoint kr = KR[i];
-        const double r = 2.0 * (double)g.scale[kr.octave];
+        const double r = 2.0 * (double)s_scale[kr.octave];
         const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
         for (int y = lo; y <= hi; ++y) {
             const int pos = atomicAdd(&cnt[y], 1);
@@ -1654,6 +1657,21 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     __shared__ int sad[16][11];
     __shared__ uint8_t sL[16][121];
     __shared__ uint8_t sR[16][231];
+    // per-octave geometry (scale, inverse scale, w, h, pitch, ws_off) in LDS: indexed by a keypoint's octave
+    // the kernel argument would be read with vector memory loads, two dependent round trips in the refine
+    __shared__ float s_sc[kMaxLevels], s_isc[kMaxLevels];
+    __shared__ int s_w[kMaxLevels], s_h[kMaxLevels], s_pitch[kMaxLevels];
+    __shared__ int64_t s_wsoff[kMaxLevels];
+    if (threadIdx.x < kMaxLevels) {
+        const int i = threadIdx.x;
+        s_sc[i] = g.scale[i];
+        s_isc[i] = g.inv_scale[i];
+        s_w[i] = g.lv[i].w;
+        s_h[i] = g.lv[i].h;
+        s_pitch[i] = g.lv[i].pitch;
+        s_wsoff[i] = g.lv[i].ws_off;
+    }
+    __syncthreads();
     int bx, pr;
     xcd_block(bx, pr);  // a pair's blocks read the same pyramids, descriptors and buckets: one L2
     const int lane = threadIdx.x & 63, sl = lane & 15;
@@ -1719,12 +1737,12 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     bool do_sad = false;
     if (refine) {
         const int oct = kl.octave;
-        const double isf = (double)g.inv_scale[oct];
+        const double isf = (double)s_isc[oct];
         const float uR0 = KR[bidx].x;
         const int scaleduL = (int)py_round((double)kl.x * isf);
         const int scaledvL = (int)py_round((double)kl.y * isf);
         scaleduR0 = (int)py_round((double)uR0 * isf);
-        const int lw = g.lv[oct].w, lh = g.lv[oct].h;
+        const int lw = s_w[oct], lh = s_h[oct];
         const uint8_t *lvlL, *lvlR;
         int lstride;
         if (oct == 0) {
@@ -1732,9 +1750,9 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             lvlR = A.lvl0R + pr * A.lvl0_stride;
             lstride = g.W;
         } else {
-            lvlL = A.wsL + pr * A.ws_stride + g.lv[oct].ws_off;
-            lvlR = A.wsR + pr * A.ws_stride + g.lv[oct].ws_off;
-            lstride = g.lv[oct].pitch;
+            lvlL = A.wsL + pr * A.ws_stride + s_wsoff[oct];
+            lvlR = A.wsR + pr * A.ws_stride + s_wsoff[oct];
+            lstride = s_pitch[oct];
         }
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
@@ -1772,7 +1790,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             const int d1 = sad[kq][bi - 1], d2 = sad[kq][bi], d3 = sad[kq][bi + 1];
             const float deltaR = __fdiv_rn((float)(d1 - d3), (float)(2 * (d1 + d3 - 2 * d2)));
             if (!(deltaR < -1.f || deltaR > 1.f)) {
-                const float bestuR = __fmul_rn(g.scale[kl.octave], __fadd_rn((float)(scaleduR0 + bi - 5), deltaR));
+                const float bestuR = __fmul_rn(s_sc[kl.octave], __fadd_rn((float)(scaleduR0 + bi - 5), deltaR));
                 const float disparity = __fsub_rn(kl.x, bestuR);
                 if (0.f <= disparity && disparity < A.maxD) {
                     if (disparity <= 0.f) {  // Python-double substitution, recomputed on the host
