@@ -646,6 +646,36 @@ __device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
     return (x < mx ? 0 : 1) + (y < my ? 0 : 2);
 }
 
+// Child-quadrant counts of one octree pass: bins 4 p + quadrant of every candidate k whose node p is
+// divided (div(p)).  Thread t takes the contiguous candidates [t * per, (t + 1) * per), two per step with
+// their LDS loads in flight together, and adds a run length to the LDS counter whenever the bin changes.
+template <typename Div>
+__device__ __forceinline__ void octree_count_runs(int K, int t, const uint16_t* kn, const uint32_t* kd, Div div,
+                                                  const uint64_t* box, int* bins) {
+    const int per = (K + kOctThreads - 1) / kOctThreads;
+    const int kb = min(t * per, K), ke = min(kb + per, K);
+    int cur = -1, run = 0;
+    auto add = [&](int p, uint32_t key) {
+        if (!div(p)) return;
+        const int b = 4 * p + quad_of(key, box[p]);
+        if (b != cur) {
+            if (run) atomicAdd(&bins[cur], run);
+            cur = b;
+            run = 0;
+        }
+        ++run;
+    };
+    int k = kb;
+    for (; k + 1 < ke; k += 2) {
+        const int p0 = kn[k], p1 = kn[k + 1];
+        const uint32_t k0 = kd[k], k1 = kd[k + 1];
+        add(p0, k0);
+        add(p1, k1);
+    }
+    if (k < ke) add(kn[k], kd[k]);
+    if (run) atomicAdd(&bins[cur], run);
+}
+
 __device__ __forceinline__ uint64_t pack_box(int x0, int y0, int x1, int y1) {
     return (uint64_t)(uint16_t)x0 | ((uint64_t)(uint16_t)y0 << 16) | ((uint64_t)(uint16_t)x1 << 32) |
            ((uint64_t)(uint16_t)y1 << 48);
@@ -843,27 +873,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                 for (int i = t; i < 4 * S; i += kOctThreads) d.cnt4[i] = 0;
                 if (t == 0) s_nexp = 0;
                 __syncthreads();
-                // 4 candidates per step so their LDS chains overlap; few counters: aggregate per wave
-                for (int k0 = 0; k0 < K; k0 += 4 * kOctThreads) {
-                    int b[4];
-                    bool a[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int k = k0 + u * kOctThreads + t;
-                        b[u] = 0;
-                        a[u] = false;
-                        if (k < K) {
-                            const int p = kn[k];
-                            a[u] = cnt[p] > 1;
-                            b[u] = 4 * p + quad_of(kd[k], box[p]);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (4 * S <= 64) wave_bin_add(d.cnt4, b[u], a[u]);
-                        else if (a[u]) atomicAdd(&d.cnt4[b[u]], 1);
-                    }
-                }
+                // each thread counts a contiguous run of candidates: consecutive candidates (cell order)
+                // mostly fall into the same child, so a thread adds one run length per change of bin instead
+                // of one LDS atomic per candidate on a handful of hot counters
+                octree_count_runs(K, t, kn, kd, [&](int p) { return cnt[p] > 1; }, box, d.cnt4);
                 __syncthreads();
                 mark(9 + 4 * iter);
                 for (int p = t; p < S; p += kOctThreads) {
@@ -940,21 +953,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                 for (int p = t; p < S; p += kOctThreads) d.proc[p] = 0;
                 if (t == 0) s_P = 0x7fffffff;
                 __syncthreads();
-                for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {
-                    int b[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int k = k0 + u * kOctThreads;
-                        b[u] = -1;
-                        if (k < K) {
-                            const int p = kn[k];
-                            if (p < C && cnt[p] > 1) b[u] = 4 * p + quad_of(kd[k], box[p]);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (b[u] >= 0) atomicAdd(&d.cnt4[b[u]], 1);
-                }
+                octree_count_runs(K, t, kn, kd, [&](int p) { return p < C && cnt[p] > 1; }, box, d.cnt4);
                 for (int p = t; p < C; p += kOctThreads) d.sa[p] = cnt[p] > 1;
                 __syncthreads();
                 const int M = block_excl_scan(d.sa, C, scan_tmp);
