@@ -818,15 +818,22 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
         const int nIni = L.n_ini;
         for (int i = t; i < 4 * NC; i += kOctThreads) d.cnt4[i] = 0;
         __syncthreads();
-        for (int k0 = 0; k0 < K; k0 += kOctThreads) {  // wave-uniform trip count (ballots inside)
-            const int k = k0 + t;
-            int col = 0;
-            if (k < K) {
+        {  // contiguous candidate runs per thread, one LDS atomic per change of column (octree_count_runs)
+            const int per = (K + kOctThreads - 1) / kOctThreads;
+            const int kb = min(t * per, K), ke = min(kb + per, K);
+            int cur = -1, run = 0;
+            for (int k = kb; k < ke; ++k) {
                 const int x = (int)(kd[k] & 0xFFFu) - kBorder;
-                col = min((int)((float)x / L.hx), nIni - 1);
+                const int col = min((int)((float)x / L.hx), nIni - 1);
                 kn[k] = (uint16_t)col;
+                if (col != cur) {
+                    if (run) atomicAdd(&d.cnt4[cur], run);
+                    cur = col;
+                    run = 0;
+                }
+                ++run;
             }
-            wave_bin_add(d.cnt4, col, k < K);
+            if (run) atomicAdd(&d.cnt4[cur], run);
         }
         __syncthreads();
         if (t == 0) {
@@ -1064,9 +1071,22 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
         uint32_t* best = (uint32_t*)d.cnt4;
         for (int p = t; p < S; p += kOctThreads) best[p] = 0;
         __syncthreads();
-        for (int k = t; k < K; k += kOctThreads) {
-            const int p = kn[k];
-            if (p < S) atomicMax(&best[p], (kd[k] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
+        {  // contiguous candidate runs per thread: one LDS atomicMax per change of node
+            const int per = (K + kOctThreads - 1) / kOctThreads;
+            const int kb = min(t * per, K), ke = min(kb + per, K);
+            int cur = -1;
+            uint32_t m = 0;
+            for (int k = kb; k < ke; ++k) {
+                const int p = kn[k];
+                const uint32_t v = (kd[k] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k);
+                if (p != cur) {
+                    if (cur >= 0 && cur < S) atomicMax(&best[cur], m);
+                    cur = p;
+                    m = 0;
+                }
+                m = max(m, v);
+            }
+            if (cur >= 0 && cur < S) atomicMax(&best[cur], m);
         }
         __syncthreads();
         for (int p = t; p < S; p += kOctThreads) {
