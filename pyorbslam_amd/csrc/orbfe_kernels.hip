@@ -624,20 +624,6 @@ struct OctLds {
     uint16_t* kn;
 };
 
-// atomicAdd(&bins[b], 1) for every active lane, aggregated per distinct bin of the wave (ballot +
-// popcount, one LDS atomic per bin): for the first octree passes, where thousands of candidates share
-// a handful of counters and plain LDS atomics serialize.
-__device__ __forceinline__ void wave_bin_add(int* bins, int b, bool active) {
-    uint64_t todo = __ballot(active);
-    while (todo) {
-        const int leader = __builtin_ctzll(todo);
-        const int lb = __shfl(b, leader, 64);
-        const uint64_t same = __ballot(active && b == lb) & todo;
-        if ((threadIdx.x & 63) == leader) atomicAdd(&bins[lb], __popcll(same));
-        todo &= ~same;
-    }
-}
-
 __device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
     const int x = (int)(key & 0xFFFu) - kBorder, y = (int)((key >> 12) & 0xFFFu) - kBorder;
     const int x0 = (int16_t)(box & 0xFFFF), y0 = (int16_t)((box >> 16) & 0xFFFF);
