@@ -308,8 +308,9 @@ __device__ __forceinline__ fd_h2 fd_pair(const uint32_t* q) {  // u16 pair at co
 template <int S>
 __device__ __forceinline__ fd_s2 fast_bound_pair(const uint32_t* R) {
     const fd_h2 c0 = fd_pair<0>(R + 3 * S), c1 = fd_pair<3>(R), c2 = fd_pair<0>(R - 3 * S), c3 = fd_pair<-3>(R);
-    const fd_h2 a = fd_min(fd_min3(fd_max(c0, c1), fd_max(c1, c2), fd_max(c2, c3)), fd_max(c3, c0));
-    const fd_h2 b = fd_max(fd_max3(fd_min(c0, c1), fd_min(c1, c2), fd_min(c2, c3)), fd_min(c3, c0));
+    // every cycle edge joins an even and an odd cardinal: min_edges max = max(min(c0, c2), min(c1, c3))
+    const fd_h2 a = fd_max(fd_min(c0, c2), fd_min(c1, c3));
+    const fd_h2 b = fd_min(fd_max(c0, c2), fd_max(c1, c3));
     const fd_s2 v = __builtin_bit_cast(fd_s2, R[0]);
     return __builtin_elementwise_max(v - fd_s(a), fd_s(b) - v);
 }
@@ -322,8 +323,10 @@ __device__ __forceinline__ void fast_bound_quad(const uint32_t* R, fd_s2& bA, fd
     const uint32_t u0 = R[-3 * S], u1 = R[-3 * S + 1], d0 = R[3 * S], d1 = R[3 * S + 1];
     auto bound = [](uint32_t v, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
         const fd_h2 h0 = fd_h(c0), h1 = fd_h(c1), h2 = fd_h(c2), h3 = fd_h(c3);
-        const fd_h2 a = fd_min(fd_min3(fd_max(h0, h1), fd_max(h1, h2), fd_max(h2, h3)), fd_max(h3, h0));
-        const fd_h2 b = fd_max(fd_max3(fd_min(h0, h1), fd_min(h1, h2), fd_min(h2, h3)), fd_min(h3, h0));
+        // min over the 4 cycle edges (i, i + 1) of max(h_i, h_i+1): every edge joins an even and an odd
+        // cardinal, so it is max(min(h0, h2), min(h1, h3)) (3 ops instead of 6); dually for b
+        const fd_h2 a = fd_max(fd_min(h0, h2), fd_min(h1, h3));
+        const fd_h2 b = fd_min(fd_max(h0, h2), fd_max(h1, h3));
         const fd_s2 vs = __builtin_bit_cast(fd_s2, v);
         return __builtin_elementwise_max(vs - fd_s(a), fd_s(b) - vs);
     };
