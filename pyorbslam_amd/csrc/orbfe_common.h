@@ -43,6 +43,9 @@ struct LevelGeo {
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
     int64_t blur_off;    // byte offset of the blurred level inside an image's blur workspace
     int blur_tile0;      // first k_blur tile of this level (64 x 32 tiles)
+    // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;
+    // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
+    int rs_ngrp, rs_nsrc, rs_sp;
 };
 
 // One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.

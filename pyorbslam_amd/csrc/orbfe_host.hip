@@ -340,13 +340,17 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.rs_sp = g.W;
     g.rs_ngrp = 4;
     for (int l = 1; l < L; ++l) {
-        const LevelGeo& Lg = g.lv[l];
+        LevelGeo& Lg = g.lv[l];
+        Lg.rs_nsrc = 1;
         for (int dy0 = 0; dy0 < Lg.h; dy0 += 8) {
             const int dy1 = std::min(dy0 + 8, Lg.h);
-            g.rs_nsrc = std::max(g.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
+            Lg.rs_nsrc = std::max(Lg.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
         }
-        if (l >= 2) g.rs_sp = std::max(g.rs_sp, g.lv[l - 1].pitch);
-        g.rs_ngrp = std::max(g.rs_ngrp, ((Lg.w + 3) / 4 + 3) & ~3);
+        Lg.rs_sp = l >= 2 ? g.lv[l - 1].pitch : g.W;
+        Lg.rs_ngrp = ((Lg.w + 3) / 4 + 3) & ~3;
+        g.rs_nsrc = std::max(g.rs_nsrc, Lg.rs_nsrc);
+        g.rs_sp = std::max(g.rs_sp, Lg.rs_sp);
+        g.rs_ngrp = std::max(g.rs_ngrp, Lg.rs_ngrp);
     }
     if ((int64_t)g.rs_ngrp * 36 + 128 + (int64_t)g.rs_nsrc * g.rs_sp + 16 > 150 * 1024)
         throw Error(ORBFE_EINVAL, "image too wide for the k_resize band staging (LDS)");

@@ -164,12 +164,12 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
                                                 uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
-    uint4* s_sel = (uint4*)rs_lds;                       // g.rs_ngrp groups each
-    uint4* s_aa = s_sel + g.rs_ngrp;
-    int* s_sx0 = (int*)(s_aa + g.rs_ngrp);
-    uint32_t* s_ry = (uint32_t*)(s_sx0 + g.rs_ngrp);     // kRsRows ResizeY as 3 dwords
-    uint32_t* s_src = s_ry + 4 * kRsRows;                // staged source rows
     const LevelGeo& L = g.lv[l];
+    uint4* s_sel = (uint4*)rs_lds;                       // L.rs_ngrp groups each
+    uint4* s_aa = s_sel + L.rs_ngrp;
+    int* s_sx0 = (int*)(s_aa + L.rs_ngrp);
+    uint32_t* s_ry = (uint32_t*)(s_sx0 + L.rs_ngrp);     // kRsRows ResizeY as 3 dwords
+    uint32_t* s_src = s_ry + 4 * kRsRows;                // staged source rows
     const LevelGeo& P = g.lv[l - 1];
     int bx, img;
     xcd_block(bx, img);  // neighbouring bands share source rows: keep them in one L2
@@ -1891,7 +1891,8 @@ __global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restric
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s, int variant) {
     dim3 grid((g.lv[l].h + kRsRows - 1) / kRsRows, n_images);
-    const size_t lds = (size_t)g.rs_ngrp * 36 + 16 * kRsRows + (size_t)g.rs_nsrc * g.rs_sp + 16;
+    const LevelGeo& L = g.lv[l];  // LDS sized for this level (tables + its bands' source rows)
+    const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
     auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();
