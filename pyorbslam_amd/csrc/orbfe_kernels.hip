@@ -615,6 +615,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
 //   kd[g.oct_keys] u32 | kn[g.oct_keys] u16   (the candidates, when the level has at most g.oct_keys; else they
 //   stay in the global kd/kn arrays)
 constexpr int kOctThreads = 512;   // 8 waves: the per-pass candidate loops are latency chains
+constexpr int kOctGather = 16;     // candidate slot loads in flight per thread in the gather
 struct OctLds {
     uint64_t *box0, *box1;
     int *cnt0, *cnt1;
@@ -764,10 +765,12 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
             for (int i = t; i < ncell; i += kOctThreads)
                 for (int k = d.coff[i]; k < d.coff[i + 1]; ++k) kn[k] = (uint16_t)i;
             __syncthreads();
-            for (int k0 = t; k0 < K; k0 += 4 * kOctThreads) {  // 4 keys per step: their slot loads overlap
-                uint32_t v[4];
+            // kOctGather keys per thread and step (coalesced across threads): a level's slot loads are one
+            // round trip, not one per 4 keys
+            for (int k0 = t; k0 < K; k0 += kOctGather * kOctThreads) {
+                uint32_t v[kOctGather];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < kOctGather; ++u) {
                     const int k = k0 + u * kOctThreads;
                     v[u] = 0;
                     if (k < K) {
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < kOctGather; ++u)
                     if (k0 + u * kOctThreads < K) kd[k0 + u * kOctThreads] = v[u];
             }
             __syncthreads();  // pass 2 clears cnt4 (the slot offsets) and rewrites kn
