@@ -1773,7 +1773,11 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             sheared_row(lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, &sR[kq][sl * 21]);
         }
     }
-    __syncthreads();
+    // sL / sR / sad are per 16-lane group, i.e. per wavefront: a wavefront barrier orders them (the
+    // wavefronts of the block need not wait for each other's searches)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (do_sad) {
         const int lc = sL[kq][60];  // IL[5][5]
         // 11 shifts x 11 rows = 121 row sums of 11 |(IL - IL[5,5]) - (IR - IR[5,5])| terms
@@ -1789,7 +1793,9 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
             atomicAdd(&sad[kq][s], acc);
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (do_sad && sl == 0) {
         int bi = 0, bd = sad[kq][0];
         for (int s = 1; s < 11; ++s)
