@@ -59,6 +59,7 @@ struct CellGeo {
 // Resize column entry.
 // k_blur output tile (the host counts tiles per level with the same numbers)
 constexpr int kBlurTX = 64, kBlurTY = 58;
+constexpr int kRsRows = 16;  // k_resize output rows per workgroup (band)
 // k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
 constexpr int kOctKeys = 7424;
 

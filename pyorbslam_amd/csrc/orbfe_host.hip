@@ -335,15 +335,15 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.ncells = (int)c.cells.size();
     g.kp_cap = kp_off;
     g.lvl_kp_cap = kp_off;
-    // k_resize geometry: source rows per 8-row output band, source row stride, groups per row
+    // k_resize geometry: source rows per kRsRows-row output band, source row stride, groups per row
     g.rs_nsrc = 1;
     g.rs_sp = g.W;
     g.rs_ngrp = 4;
     for (int l = 1; l < L; ++l) {
         LevelGeo& Lg = g.lv[l];
         Lg.rs_nsrc = 1;
-        for (int dy0 = 0; dy0 < Lg.h; dy0 += 8) {
-            const int dy1 = std::min(dy0 + 8, Lg.h);
+        for (int dy0 = 0; dy0 < Lg.h; dy0 += kRsRows) {
+            const int dy1 = std::min(dy0 + kRsRows, Lg.h);
             Lg.rs_nsrc = std::max(Lg.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
         }
         Lg.rs_sp = l >= 2 ? g.lv[l - 1].pitch : g.W;

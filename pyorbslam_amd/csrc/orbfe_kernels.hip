@@ -156,7 +156,6 @@ __device__ int block_sum(int v, int* red) {
 //  * compute: per group and row, 2 x (3 LDS dwords, 2 v_alignbyte, 4 v_perm + 4 v_dot2_u32_u16) for the
 //    horizontal taps, then OpenCV's vertical rounding; one aligned dword store per 4 output pixels.
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-constexpr int kRsRows = 8;
 constexpr int kRsSlots = 16;  // staged dwords per thread per pass
 
 template <int V>  // V: 0 full kernel; ablations for tools/microbench.py: 1 staging only, 2 compute only
