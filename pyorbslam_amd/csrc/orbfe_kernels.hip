@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
             if (o[k] >= 0) sb[o[k]] = v[k];
     }
     __syncthreads();
-    constexpr uint32_t K1 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K2 = 48u | (34u << 8) | (18u << 16);
+    auto w4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | (b << 8) | (c << 16) | (d << 24); };
     // horizontal: (row pair m, group of 4 columns gx): 32 x 16 items, 2 per thread
 #pragma unroll
     for (int j = 0; j < (kBlurWR / 2) * (kBlurTX / 4) / 256; ++j) {
@@ -1275,13 +1275,20 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
         for (int rr = 0; rr < 2; ++rr) {
             const uint32_t* q = src + (2 * m + rr) * kBlurSD + gx;
             const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
-            h[rr][0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), K1,
-                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), K2, 0u, false), false);
-            h[rr][1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), K1,
-                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), K2, 0u, false), false);
-            h[rr][2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), K1,
-                                              __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), K2, 0u, false), false);
-            h[rr][3] = __builtin_amdgcn_udot4(d1, K1, __builtin_amdgcn_udot4(d2, K2, 0u, false), false);
+            // output i reads window bytes 1 + i .. 7 + i of (d0, d1, d2): the 7 taps spread over the aligned
+            // dwords with shifted byte weights (10 v_dot4 per 4 outputs, no v_alignbyte)
+            h[rr][0] = __builtin_amdgcn_udot4(d1, w4(56, 48, 34, 18), __builtin_amdgcn_udot4(d0, w4(0, 18, 34, 48), 0u, false),
+                                              false);
+            h[rr][1] = __builtin_amdgcn_udot4(
+                d2, w4(18, 0, 0, 0),
+                __builtin_amdgcn_udot4(d1, w4(48, 56, 48, 34), __builtin_amdgcn_udot4(d0, w4(0, 0, 18, 34), 0u, false), false),
+                false);
+            h[rr][2] = __builtin_amdgcn_udot4(
+                d2, w4(34, 18, 0, 0),
+                __builtin_amdgcn_udot4(d1, w4(34, 48, 56, 48), __builtin_amdgcn_udot4(d0, w4(0, 0, 0, 18), 0u, false), false),
+                false);
+            h[rr][3] = __builtin_amdgcn_udot4(d2, w4(48, 34, 18, 0), __builtin_amdgcn_udot4(d1, w4(18, 34, 48, 56), 0u, false),
+                                              false);
         }
         *(uint4*)(hor + m * kBlurTX + 4 * gx) = uint4{h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
                                                        h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
