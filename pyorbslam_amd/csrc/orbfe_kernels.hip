@@ -303,17 +303,6 @@ __device__ __forceinline__ fd_h2 fd_pair(const uint32_t* q) {  // u16 pair at co
     else return fd_h(__builtin_amdgcn_alignbyte(q[(DX + 1) / 2], q[(DX - 1) / 2], 2));
 }
 
-// Upper bound P of M for the pixel pair at dword R (row stride S dwords), as int16 x2.
-template <int S>
-__device__ __forceinline__ fd_s2 fast_bound_pair(const uint32_t* R) {
-    const fd_h2 c0 = fd_pair<0>(R + 3 * S), c1 = fd_pair<3>(R), c2 = fd_pair<0>(R - 3 * S), c3 = fd_pair<-3>(R);
-    // every cycle edge joins an even and an odd cardinal: min_edges max = max(min(c0, c2), min(c1, c3))
-    const fd_h2 a = fd_max(fd_min(c0, c2), fd_min(c1, c3));
-    const fd_h2 b = fd_min(fd_max(c0, c2), fd_max(c1, c3));
-    const fd_s2 v = __builtin_bit_cast(fd_s2, R[0]);
-    return __builtin_elementwise_max(v - fd_s(a), fd_s(b) - v);
-}
-
 // Upper bounds of the two adjacent pixel pairs at dwords R and R + 1 (pixels x .. x + 3), sharing the
 // cardinal rows: 6 dwords of the centre row, 2 above, 2 below.
 template <int S>
