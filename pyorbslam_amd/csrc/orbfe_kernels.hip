@@ -271,18 +271,20 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 // u16 0x3C00 | p, normal f16 numbers in [1, 2) ordered exactly like p, so v_pk_maximum3/minimum3_f16
 // are exact and differences of the raw u16 bits are differences of p.
 //  1. ROI -> LDS (u16, pitch RP, ROI column c at index c + 1 so even window columns are dword
-//     aligned): 16 lanes per row read 16 dwords from the 4-byte aligned start of column -1, re-aligned
-//     with v_alignbyte and widened with v_perm; all loads issued before the first wait.
+//     aligned): 16 lanes per row each read one dword from the 4-byte aligned start of column -1, take
+//     the next dword from the neighbour lane (DPP), re-align with v_alignbyte and widen with v_perm; the
+//     next cell's loads are in flight during this cell's compute.
 //  2. Pre-test, every pair: P = max(v - min_k max(c_k, c_k+1), max_k min(c_k, c_k+1) - v) over the
 //     circularly adjacent cardinal pairs (circle points 0, 4, 8, 12) bounds M from above, because every
-//     arc of 9 contains such a pair.  Pairs with P <= tq = min(iniTh, minTh) in both pixels have M <= tq:
+//     arc of 9 contains such a pair (computed as max(v - max(min(c0, c2), min(c1, c3)), ...): every
+//     cycle edge joins an even and an odd cardinal).  Pairs with P <= tq = min(iniTh, minTh) in both pixels have M <= tq:
 //     neither corners nor relevant NMS neighbours at either threshold; they keep M = 0.  The others are
 //     queued in row-major order (ballot + mbcnt).  (Queueing single pixels halves the M work per pixel
 //     but not per cell: a cell's queue is a few 64-entry steps either way, measured slower.)
 //  3. Exact M of the queued pairs -> a u8 M map with a zero border (half the LDS of a u16 map: detect is
-//     occupancy-bound, one 64-thread workgroup per wave); pixels with M > max(tq, 1) are queued
-//     (row-major: two ballots per step) for NMS.
-//  4. NMS over that queue.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the
+//     occupancy-bound, one 64-thread workgroup per wave); pairs with a pixel above max(tq, 1) are
+//     compacted in place into the same queue (row-major) for NMS.
+//  4. NMS over that queue, two pixels per lane.  For t >= 1, "score > every 8-neighbour's score at t" (neighbours outside the
 //     window or not corners at t score 0) is equivalent to M > t and M > max(8-neighbour M): a neighbour
 //     with M <= t is below M anyway.  So the local-max test is threshold independent: one pass decides
 //     iniTh and minTh together, and the iniTh -> minTh fallback (ORBextractor.cpp:811-815) only picks
