@@ -1285,38 +1285,48 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
                                                        h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
     }
     __syncthreads();
-    // vertical: (output row pair n, group gx): window rows 2n+3, 2n+4 = tile rows 2n, 2n+1
+    // vertical: (row quad n2, group gx): tile rows 4 n2 .. 4 n2 + 3 from the 5 interleaved row-pair dwords
+    // P(2 n2) .. P(2 n2 + 4) (rows 4 n2, 4 n2 + 1 use P(0..3), rows 4 n2 + 2, 4 n2 + 3 use P(1..4)): one item
+    // per thread (15 x 16 items), 5 LDS reads per 4 output rows
     uint8_t* dstimg = blur + (int64_t)img * g.blur_bytes + L.blur_off;
     auto w2 = [](uint32_t a, uint32_t b) { return __builtin_bit_cast(us2, a | (b << 16)); };
-    for (int it = t; it < (kBlurTY / 2) * (kBlurTX / 4); it += 256) {
-        const int n = it >> 4, gx = it & 15;
-        const int y = Y0 + 2 * n, x = X0 + 4 * gx;
+    constexpr int kPairs = kBlurWR / 2;  // row pairs in hor
+    for (int it = t; it < ((kBlurTY + 3) / 4) * (kBlurTX / 4); it += 256) {
+        const int n2 = it >> 4, gx = it & 15;
+        const int y = Y0 + 4 * n2, x = X0 + 4 * gx;
         if (y >= L.h || x >= L.w) continue;
-        uint4 P[4];
+        const int n = 2 * n2;
+        uint4 P[5];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) P[k] = *(const uint4*)(hor + (n + k) * kBlurTX + 4 * gx);
-        uint32_t e = 0, o = 0;
+        for (int k = 0; k < 5; ++k)
+            P[k] = n + k < kPairs ? *(const uint4*)(hor + (n + k) * kBlurTX + 4 * gx) : uint4{0u, 0u, 0u, 0u};
+        uint32_t out[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t p0 = (&P[0].x)[c], p1 = (&P[1].x)[c], p2 = (&P[2].x)[c], p3 = (&P[3].x)[c];
-            uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(18, 34), 32768u, false);
-            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(48, 56), a, false);
-            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(48, 34), a, false);
-            a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(18, 0), a, false);
-            uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(0, 18), 32768u, false);
-            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(34, 48), b, false);
-            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(56, 48), b, false);
-            b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(34, 18), b, false);
-            e |= (a >> 16) << (8 * c);
-            o |= (b >> 16) << (8 * c);
+        for (int h2 = 0; h2 < 2; ++h2) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t p0 = (&P[h2].x)[c], p1 = (&P[h2 + 1].x)[c], p2 = (&P[h2 + 2].x)[c], p3 = (&P[h2 + 3].x)[c];
+                uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(18, 34), 32768u, false);
+                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(48, 56), a, false);
+                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(48, 34), a, false);
+                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(18, 0), a, false);
+                uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(0, 18), 32768u, false);
+                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(34, 48), b, false);
+                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(56, 48), b, false);
+                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(34, 18), b, false);
+                out[2 * h2] |= (a >> 16) << (8 * c);
+                out[2 * h2 + 1] |= (b >> 16) << (8 * c);
+            }
         }
-        // rows are padded to a 16-byte pitch, so the dwords never leave the row's allocation
+        // rows are padded to a 16-byte pitch, so the dwords never leave the row's allocation; rows past the
+        // tile (the last quad of a 58-row tile) or the level are not stored
         if (probe == 1) {  // microbench probe: no stores unless the value is impossible
-            if (e == 0x12345678u && o == 0x9abcdef0u) *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = e;
+            if (out[0] == 0x12345678u && out[1] == 0x9abcdef0u) *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = out[0];
             continue;
         }
-        *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = e;
-        if (y + 1 < L.h) *(uint32_t*)(dstimg + (int64_t)(y + 1) * L.pitch + x) = o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (4 * n2 + r < kBlurTY && y + r < L.h) *(uint32_t*)(dstimg + (int64_t)(y + r) * L.pitch + x) = out[r];
     }
 }
 
