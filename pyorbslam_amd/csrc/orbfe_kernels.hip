@@ -1161,8 +1161,9 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 //  * horizontal: 4 adjacent pixels of 2 rows per thread step, each tap sum = 2 x v_dot4_u32_u8 over
 //    v_alignbyte windows (weights 18,34,48,56 | 48,34,18,0); stored row-pair interleaved, so a dword
 //    holds (H[2m][x], H[2m+1][x]).
-//  * vertical: output rows 2n+3 and 2n+4 of the window from the 4 interleaved dwords P(n) .. P(n+3),
-//    4 x v_dot2_u32_u16 each with the +2^15 rounding as the accumulator seed; 2 aligned dword stores.
+//  * vertical: tile rows 4q .. 4q+3 from the 5 interleaved dwords P(2q) .. P(2q+4) (1.25 LDS reads per
+//    output row), 4 x v_dot2_u32_u16 per row with the +2^15 rounding as the accumulator seed; 4 aligned
+//    dword stores.
 constexpr int kBlurWR = kBlurTY + 6;        // staged window rows
 static_assert((kBlurWR / 2) * (kBlurTX / 4) % 256 == 0, "horizontal items: a whole number per thread");
 // slot / 18 as a 24-bit multiply and shift, exact for every staging slot of the window
