@@ -1158,9 +1158,9 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 //  * staging: the 64-row x 72-column input window (rows Y0-3 .., columns X0-4 ..) as 18 re-aligned dwords
 //    per row, all loads issued before the first wait; rows go through reflect-101, and the <= 3 columns
 //    left of 0 / right of w-1 of edge tiles are patched in LDS from their reflect-101 sources.
-//  * horizontal: 4 adjacent pixels of 2 rows per thread step, each tap sum = 2 x v_dot4_u32_u8 over
-//    v_alignbyte windows (weights 18,34,48,56 | 48,34,18,0); stored row-pair interleaved, so a dword
-//    holds (H[2m][x], H[2m+1][x]).
+//  * horizontal: 4 adjacent pixels of 2 rows per thread step from 3 aligned LDS dwords per row, 10
+//    v_dot4_u32_u8 with shifted byte weights per 4 outputs (no v_alignbyte); stored row-pair interleaved,
+//    so a dword holds (H[2m][x], H[2m+1][x]).
 //  * vertical: tile rows 4q .. 4q+3 from the 5 interleaved dwords P(2q) .. P(2q+4) (1.25 LDS reads per
 //    output row), 4 x v_dot2_u32_u16 per row with the +2^15 rounding as the accumulator seed; 4 aligned
 //    dword stores.
