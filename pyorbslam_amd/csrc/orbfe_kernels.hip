@@ -1156,7 +1156,7 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // bit-exact 8U fixed-point path: out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
 // One 256-thread workgroup per kBlurTX x kBlurTY output tile.
 //  * staging: the 64-row x 72-column input window (rows Y0-3 .., columns X0-4 ..) as 18 re-aligned dwords
-//    per row, all loads issued before the first wait; rows go through reflect-101, and the <= 3 columns
+//    per row, 3 per dwordx4 load, all loads issued before the first wait; rows go through reflect-101, and the <= 3 columns
 //    left of 0 / right of w-1 of edge tiles are patched in LDS from their reflect-101 sources.
 //  * horizontal: 4 adjacent pixels of 2 rows per thread step from 3 aligned LDS dwords per row, 10
 //    v_dot4_u32_u8 with shifted byte weights per 4 outputs (no v_alignbyte); stored row-pair interleaved,
@@ -1166,10 +1166,6 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 //    dword stores.
 constexpr int kBlurWR = kBlurTY + 6;        // staged window rows
 static_assert((kBlurWR / 2) * (kBlurTX / 4) % 256 == 0, "horizontal items: a whole number per thread");
-// slot / 18 as a 24-bit multiply and shift, exact for every staging slot of the window
-constexpr uint32_t kBlurDiv18Sh = kBlurWR * 18 <= 1152 ? 16 : 17;
-constexpr uint32_t kBlurDiv18 = kBlurDiv18Sh == 16 ? 3641u : 7282u;
-static_assert(kBlurWR * 18 <= 2304, "staging slot division range");
 constexpr int kBlurWD = (kBlurTX + 8) / 4;  // staged dwords per row (18)
 constexpr int kBlurSD = 20;                 // LDS pitch of a staged row, dwords
 
@@ -1194,11 +1190,10 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    constexpr int NS = (kBlurWR * kBlurWD + 255) / 256;
-    // staging: buffer dwordx2 loads at 32-bit offsets, the resource bounded by the level's extent (reads
-    // past it return 0, never fault); slot -> (row, dword) by a 24-bit multiply (slot / 18 ==
-    // (slot * 3641) >> 16 for slot < 1152); rows through reflect-101 only on tiles that reach past the
-    // top or bottom; dwords left of column 0 or right of w-1 are skipped (patched from LDS below)
+    // staging: one buffer dwordx4 load per 3 staged dwords (6 slots per row, 2 loads per thread) at 32-bit
+    // offsets, the resource bounded by the level's extent (reads past it return 0, never fault); rows
+    // through reflect-101 only on tiles that reach past the top or bottom; dwords left of column 0 or right
+    // of w-1 are skipped (patched from LDS below)
     {
         const bool yb = !(Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h);
         const uint64_t a64 = (uint64_t)(uintptr_t)lvl;
@@ -1207,29 +1202,43 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(uintptr_t)(((uint64_t)ahi << 32) | alo), 0, stride * L.h, 0x00020000);
         const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;
-        uint2 raw[NS];
-        uint32_t sh[NS];
-        int dst[NS];
+        // 3 staged dwords per slot from one dwordx4 load (6 slots per row)
+        constexpr int NT = (kBlurWR * (kBlurWD / 3) + 255) / 256;
+        static_assert(kBlurWD % 3 == 0, "dword triples per staged row");
+        uint4 raw[NT];
+        uint32_t sh[NT];
+        int dst[NT], xs[NT];
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
+        for (int k = 0; k < NT; ++k) {
             const uint32_t slot = (uint32_t)(t + 256 * k);
-            const uint32_t r = __umul24(slot, kBlurDiv18) >> kBlurDiv18Sh, d = slot - 18u * r;
-            const int x = X0 - 4 + 4 * (int)d;  // image column of the dword's first byte
-            raw[k] = uint2{0u, 0u};
+            const uint32_t r = slot / (uint32_t)(kBlurWD / 3), d = 3u * (slot - (uint32_t)(kBlurWD / 3) * r);
+            const int x = X0 - 4 + 4 * (int)d;  // image column of the first dword's first byte
+            raw[k] = uint4{0u, 0u, 0u, 0u};
             sh[k] = 0;
             dst[k] = -1;
-            if (slot < (uint32_t)(kBlurWR * kBlurWD) && x >= 0 && x < L.w) {
+            xs[k] = x;
+            if (slot < (uint32_t)(kBlurWR * (kBlurWD / 3)) && x < L.w) {
                 int ry = Y0 - 3 + (int)r;
                 if (yb) ry = reflect101c(ry, L.h);
-                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)x;
+                const int xl = max(x, 0);  // only the left edge tile's first triple starts left of column 0
+                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)xl;
                 sh[k] = (alo + off) & 3u;
-                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off - sh[k], 0, 0));
+                raw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off - sh[k], 0, 0));
+                if (x < 0) {  // shift the triple so that word i holds column x + 4 i (word 0 is skipped below)
+                    raw[k] = uint4{0u, raw[k].x, raw[k].y, raw[k].z};
+                }
                 dst[k] = (int)(r * kBlurSD + d);
             }
         }
 #pragma unroll
-        for (int k = 0; k < NS; ++k)
-            if (dst[k] >= 0) src[dst[k]] = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh[k]);
+        for (int k = 0; k < NT; ++k)
+            if (dst[k] >= 0) {
+                const uint32_t w[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (xs[k] + 4 * i >= 0 && xs[k] + 4 * i < L.w)
+                        src[dst[k] + i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh[k]);
+            }
     }
     const bool left = X0 == 0, right = X0 + kBlurTX + 4 > L.w;
     if (left || right) {  // patch the reflected columns (sources lie inside the window, never patched)
