@@ -187,6 +187,11 @@ int orbfe_hamming_search(orbfe_handle h, const uint8_t* query_desc, int32_t n_qu
 int orbfe_hamming_csr(orbfe_handle h, const uint8_t* query_desc, int32_t n_query, const uint8_t* train_desc,
                       int32_t n_train, const int32_t* cand_off, const int32_t* cand_idx, int32_t* out_dist);
 
+/* ORBMatcher.descriptor_distance for ONE pair (ORBMatcher.py:12-14; Frame.py:324-326; MapPoint.py:76-78):
+ * popcount(a ^ b) over 32 bytes, computed on the host (a device round trip costs more than the
+ * reference's ~10 us Python call; batches go through the kernels above / below). */
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t* out);
+
 /* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);

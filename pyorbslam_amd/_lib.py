@@ -65,6 +65,7 @@ SIGNATURES = {
                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "orbfe_hamming_csr": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                           C.c_void_p],
+    "orbfe_descriptor_distance": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],
     "orbfe_hamming_matrix": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p],
     "orbfe_profile_begin": [C.c_void_p, C.c_int32],
     "orbfe_profile_read": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],

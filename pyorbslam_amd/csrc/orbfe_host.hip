@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -81,9 +82,12 @@ struct orbfe_ctx {
     DevBuf<uint16_t> d_bidx;
     DevBuf<float2> d_rinfo;
     int64_t bucket_cap = 0;
-    // hamming scratch
+    // hamming scratch, shared by the orbfe_hamming_* calls on this handle; they may come from several
+    // threads (the reference runs Tracking, LocalMapping and LoopClosing as threads that all call
+    // ORBMatcher / MapPoint, System.py:59-64), so those calls hold hmu for their whole duration
     DevBuf<uint8_t> d_hq, d_ht;
     DevBuf<int> d_hoff, d_hidx, d_hres;
+    std::mutex hmu;
 
     // live profiling: kProfEvents events per batch (see prof_mark)
     std::vector<hipEvent_t> prof_ev;
@@ -847,6 +851,7 @@ int orbfe_batch_fetch_stereo(orbfe_handle h, int32_t pair, float* u_right, float
         if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
         if (pair < 0 || pair >= h->last_pairs) throw Error(ORBFE_EINVAL, "pair index out of range");
         if (h->last_stream) HIPCK(hipStreamSynchronize(h->last_stream));
+        check_overflow(*h);
         int n = 0;
         HIPCK(hipMemcpy(&n, h->d_count.p + 2 * pair, sizeof(int), hipMemcpyDeviceToHost));
         *n_out = n;
@@ -859,12 +864,24 @@ int orbfe_batch_fetch_stereo(orbfe_handle h, int32_t pair, float* u_right, float
     });
 }
 
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t* out) {
+    return guarded([&] {
+        if (!a || !b || !out) throw Error(ORBFE_EINVAL, "null argument");
+        uint64_t x[4], y[4];
+        std::memcpy(x, a, 32);
+        std::memcpy(y, b, 32);
+        *out = __builtin_popcountll(x[0] ^ y[0]) + __builtin_popcountll(x[1] ^ y[1]) + __builtin_popcountll(x[2] ^ y[2]) +
+               __builtin_popcountll(x[3] ^ y[3]);
+    });
+}
+
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
         if (n_a < 0 || n_b < 0) throw Error(ORBFE_EINVAL, "negative size");
         if (n_a == 0 || n_b == 0) return;
+        std::lock_guard<std::mutex> lk(h->hmu);
         hipStream_t s = own(*h);
         h->d_hq.ensure((size_t)n_a * 32);
         h->d_ht.ensure((size_t)n_b * 32);
@@ -889,6 +906,7 @@ void hamming_run(orbfe_ctx& c, const uint8_t* q, int nq, const uint8_t* t, int n
     const int ncand = off[nq];
     for (int i = 0; i < ncand; ++i)
         if (idx[i] < 0 || idx[i] >= nt) throw Error(ORBFE_EINVAL, "candidate index out of range");
+    std::lock_guard<std::mutex> lk(c.hmu);
     hipStream_t s = own(c);
     c.d_hq.ensure((size_t)nq * 32);
     c.d_ht.ensure((size_t)std::max(nt, 1) * 32);

@@ -38,6 +38,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
 }
 
+// Buffer resource over the dword-aligned address at or below the wave-uniform p, bounded to
+// bias + nbytes bytes; *bias = p's misalignment, so byte i of p sits at resource offset bias + i and a
+// dword-aligned load covering it starts at (bias + i) & ~3 (never below the resource base).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc(const void* p, uint32_t nbytes, uint32_t* bias) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    *bias = lo & 3u;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | (lo & ~3u)), 0, nbytes + (lo & 3u),
+                                             0x00020000);
+}
+
 // Wave-wide sum (wave-uniform result): DPP quad_perm / row_ror sums inside each 16-lane row, then the
 // four row sums through v_readlane (no LDS-crossbar round trips).
 __device__ __forceinline__ int wave_sum(int v) {
@@ -1196,11 +1208,8 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
     // of w-1 are skipped (patched from LDS below)
     {
         const bool yb = !(Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h);
-        const uint64_t a64 = (uint64_t)(uintptr_t)lvl;
-        const uint32_t alo = __builtin_amdgcn_readfirstlane((uint32_t)a64);
-        const uint32_t ahi = __builtin_amdgcn_readfirstlane((uint32_t)(a64 >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)(((uint64_t)ahi << 32) | alo), 0, stride * L.h, 0x00020000);
+        uint32_t bias;
+        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
         const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;
         // 3 staged dwords per slot from one dwordx4 load (6 slots per row)
         constexpr int NT = (kBlurWR * (kBlurWD / 3) + 255) / 256;
@@ -1221,8 +1230,8 @@ __global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__
                 int ry = Y0 - 3 + (int)r;
                 if (yb) ry = reflect101c(ry, L.h);
                 const int xl = max(x, 0);  // only the left edge tile's first triple starts left of column 0
-                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)xl;
-                sh[k] = (alo + off) & 3u;
+                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)xl + bias;
+                sh[k] = off & 3u;
                 raw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off - sh[k], 0, 0));
                 if (x < 0) {  // shift the triple so that word i holds column x + 4 i (word 0 is skipped below)
                     raw[k] = uint4{0u, raw[k].x, raw[k].y, raw[k].z};
@@ -1435,9 +1444,9 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
     const int cy = min(max((int)((key >> 12) & 0xFFF), kEdge), L.h - kEdge - 1);
     const int score = key >> 24;
     // ---- intensity centroid: 18 dwords per lane, buffer loads at 32-bit offsets from the level base
-    const uint32_t off0 = (uint32_t)((cy - kHalfPatch) * stride + cx - kHalfPatch);
-    const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
-    const __amdgpu_buffer_rsrc_t lr = uniform_rsrc(lvl);
+    uint32_t lvl_bias;
+    const __amdgpu_buffer_rsrc_t lr = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &lvl_bias);
+    const uint32_t off0 = (uint32_t)((cy - kHalfPatch) * stride + cx - kHalfPatch) + lvl_bias;
     const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;  // provably 24-bit: v_mul_u32_u24, full rate
     constexpr int NW = (31 * 9 + 15) / 16;
     // slot sl + 16 k of the 31 x 9 window -> (row r, dword d), stepped without division (16 = 9 + 7);
@@ -1451,7 +1460,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
             word[k] = 0;
             if (r < 31) {
                 const uint32_t off = off0 + (uint32_t)(r & 63) * stride24;  // both operands provably 24-bit
-                word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * d - (lvl_lo & 3u), 0, 0);
+                word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * d, 0, 0);
             }
             d += 7;
             r += 1;
@@ -1497,7 +1506,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
 #pragma unroll
         for (int k = 0; k < NW; ++k) {
             if (r < 31) {
-                const int sh = (int)((lvl_lo + off0 + (uint32_t)(r & 63) * stride24) & 3u);
+                const int sh = (int)((off0 + (uint32_t)(r & 63) * stride24) & 3u);
                 const uint2 mw2 = (&s_mw[0][0])[sh * 279 + ((r & 63) << 3) + (r & 63) + d];
                 const uint32_t mw = word[k] & mw2.x;
                 a10 = __builtin_amdgcn_udot4(mw, mw2.y, a10, false);
@@ -1649,11 +1658,10 @@ __device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int 
     if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
         // the run lies inside one row of the level (the common case): 6 dword loads from the aligned
         // start, bounded to the level (reads past its end return 0), bytes re-aligned with v_alignbyte
-        const uint64_t a64 = (uint64_t)(uintptr_t)lvl;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)a64, 0, (uint32_t)(stride * h), 0x00020000);
-        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge));
-        const uint32_t sh = (uint32_t)((a64 + off) & 3u), al = off - sh;
+        uint32_t bias;
+        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * h), &bias);
+        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge)) + bias;
+        const uint32_t sh = off & 3u, al = off - sh;
         uint32_t d[7];
 #pragma unroll
         for (int k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * k, 0, 0);

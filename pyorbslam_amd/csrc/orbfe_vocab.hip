@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -48,6 +49,10 @@ struct orbfe_vocab {
     hipStream_t stream = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     float last_ms = 0.f;
+    // transform callers share one vocabulary across threads (Frame.compute_BoW on the tracking thread,
+    // KeyFrame.compute_bow on the mapping thread: Frame.py:125, KeyFrame.py:119): the scratch buffers,
+    // the stream and the events above are guarded by this mutex
+    std::mutex mu;
     ~orbfe_vocab() {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -367,6 +372,7 @@ int orbfe_vocab_transform(orbfe_vocab_handle v, const uint8_t* desc32, int64_t n
         if (!v || n < 0 || (n > 0 && (!desc32 || !word_id || !node_id || !weight)))
             throw Error(ORBFE_EINVAL, "bad argument");
         if (n == 0) return;
+        std::lock_guard<std::mutex> lk(v->mu);
         upload(*v);
         v->d_q.ensure((size_t)n * 32);
         v->d_word.ensure(n);
@@ -390,6 +396,7 @@ int orbfe_vocab_transform_device(orbfe_vocab_handle v, const uint8_t* d_desc32, 
         if (!v || n < 0 || (n > 0 && (!d_desc32 || !d_word_id || !d_node_id || !d_weight)))
             throw Error(ORBFE_EINVAL, "bad argument");
         if (reinterpret_cast<uintptr_t>(d_desc32) & 15) throw Error(ORBFE_EINVAL, "descriptors must be 16-byte aligned");
+        std::lock_guard<std::mutex> lk(v->mu);
         upload(*v);
         launch_descend(*v, d_desc32, n, nid_level, d_word_id, d_node_id, d_weight,
                        static_cast<hipStream_t>(hip_stream));
@@ -399,6 +406,7 @@ int orbfe_vocab_transform_device(orbfe_vocab_handle v, const uint8_t* d_desc32, 
 int orbfe_vocab_last_ms(orbfe_vocab_handle v, float* ms) {
     return guarded([&] {
         if (!v || !ms) throw Error(ORBFE_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lk(v->mu);
         *ms = v->last_ms;
     });
 }

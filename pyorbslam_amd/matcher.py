@@ -24,6 +24,7 @@ reads with the collected one and re-runs that query's distances on the GPU when 
 from __future__ import annotations
 
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -34,16 +35,31 @@ TH_HIGH = 100     # ORBMatcher.py:3
 TH_LOW = 50       # ORBMatcher.py:4
 HISTO_LENGTH = 30  # ORBMatcher.py:5
 
-_handle = None
+
+class _OwnedHandle:
+    """An orbfe handle (own stream + Hamming scratch) destroyed with its owner."""
+
+    def __init__(self):
+        self.h = C.c_void_p()
+        call("orbfe_create", C.byref(_lib.make_params(2000, 1.2, 8, 20, 7)), C.byref(self.h))
+
+    def __del__(self):
+        if self.h.value and _lib._lib is not None:
+            _lib.lib().orbfe_destroy(self.h)
+            self.h = C.c_void_p()
+
+
+# One handle per calling thread: the reference runs Tracking, LocalMapping and LoopClosing as threads
+# that all use ORBMatcher and MapPoint (System.py:59-64).  A thread's handle is destroyed with its
+# thread-local storage; the C side also serialises the Hamming calls of one handle (orbfe_ctx::hmu).
+_local = threading.local()
 
 
 def _h():
-    global _handle
-    if _handle is None:
-        h = C.c_void_p()
-        call("orbfe_create", C.byref(_lib.make_params(2000, 1.2, 8, 20, 7)), C.byref(h))
-        _handle = h
-    return _handle
+    o = getattr(_local, "owned", None)
+    if o is None:
+        o = _local.owned = _OwnedHandle()
+    return o.h
 
 
 def hamming_csr(queries: np.ndarray, train: np.ndarray, cand_off: np.ndarray, cand_idx: np.ndarray) -> np.ndarray:
@@ -57,6 +73,19 @@ def hamming_csr(queries: np.ndarray, train: np.ndarray, cand_off: np.ndarray, ca
         return out[:0]
     call("orbfe_hamming_csr", _h(), ptr(q), len(q), ptr(t), len(t), ptr(off), ptr(idx), ptr(out))
     return out[:int(off[-1])]
+
+
+def descriptor_distance(a, b) -> int:
+    """popcount(a ^ b) of two 32-byte descriptors (liborbfe host popcount: one pair does not pay a device
+    round trip)."""
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    if a.size != 32 or b.size != 32:
+        raise ValueError("descriptors must be 32 bytes")
+    out = C.c_int32()
+    _lib.check("orbfe_descriptor_distance", _lib.lib().orbfe_descriptor_distance(a.ctypes.data, b.ctypes.data,
+                                                                               C.byref(out)))
+    return out.value
 
 
 def hamming_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -73,9 +102,9 @@ class ORBMatcher:
         self.mfNNratio = nnratio
         self.mbCheckOrientation = checkOri
 
-    # ORBMatcher.py:12-14 (one pair; use descriptor_distances / hamming_* for batches)
+    # ORBMatcher.py:12-14 (one pair, on the host in liborbfe; use descriptor_distances / hamming_* for batches)
     def descriptor_distance(self, a, b):
-        return int(hamming_matrix(np.asarray(a).reshape(1, 32), np.asarray(b).reshape(1, 32))[0, 0])
+        return descriptor_distance(a, b)
 
     def descriptor_distances(self, A, B):
         return hamming_matrix(A, B)

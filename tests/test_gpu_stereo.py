@@ -156,3 +156,34 @@ def test_stereo_configurations_match_restatement(ci):
         sb, vb = stereo_oracle.encode(b)
         assert np.array_equal(sa, sb) and np.array_equal(va, vb)
     assert int((res["status"] > 0).sum()) > 0
+
+
+@pytest.mark.parametrize("wh", [(641, 333), (211, 157)])
+def test_batch_path_misaligned_images(wh):
+    """Odd W*H: every second image of a (2P, H, W) batch starts at an address that is not 4-byte aligned
+    (and so does the whole batch when it is a slice starting at an odd image).  The buffer loads of
+    k_blur / k_describe / k_stereo must re-align from the dword at or below the image base; results equal
+    the single-image path, whose staging buffer is aligned."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd.batch import StereoFrontEnd
+    w, h = wh
+    prm = dict(nfeatures=600, scaleFactor=1.2, nlevels=4 if w < 300 else 8, iniThFAST=20, minThFAST=7)
+    pairs = [synth.make_pair(60 + i, w, h) for i in range(3)]
+    host = np.stack([im for p in pairs for im in p] + [pairs[0][0]])  # 7 images: a spare one in front
+    host = np.concatenate([host[-1:], host[:-1]])
+    d = torch.from_numpy(np.ascontiguousarray(host)).cuda()
+    fe = StereoFrontEnd(w, h, max_pairs=3, **prm)
+    fe.enqueue(d[1:], 3)  # base = spare image + W*H bytes: odd offset
+    torch.cuda.synchronize()
+    for p, (L, R) in enumerate(pairs):
+        exL, exR = ORBextractor(**prm), ORBextractor(**prm)
+        kl, dl = exL.extract(L)
+        kr, dr = exR.extract(R)
+        bk, bd = fe.fetch_image(2 * p)
+        assert bk.tobytes() == kl.tobytes() and np.array_equal(bd, dl), f"pair {p} left"
+        bk, bd = fe.fetch_image(2 * p + 1)
+        assert bk.tobytes() == kr.tobytes() and np.array_equal(bd, dr), f"pair {p} right"
+        single = F.stereo_match_arrays(exL, exR, BF, np.float32(FX))
+        batch = fe.fetch_stereo(p)
+        for k in ("status", "u_right", "depth", "match_r"):
+            assert np.array_equal(single[k], batch[k]), (p, k)

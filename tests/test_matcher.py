@@ -81,3 +81,53 @@ def test_hamming_search_top2_matches_sequential_scan():
             elif d < b2:
                 b2, i2 = d, int(c)
         assert (bd[k], bi[k], sd[k], si[k]) == (b1, i1, b2, i2), k
+
+
+@pytest.mark.gpu
+def test_hamming_concurrent_threads():
+    """ORBMatcher / MapPoint are called from the Tracking, LocalMapping and LoopClosing threads at once
+    (System.py:59-64): concurrent hamming_csr / hamming_matrix calls at different sizes (so the scratch
+    buffers are re-allocated while the other thread runs) must each return numpy's popcounts."""
+    import threading
+    from pyorbslam_amd import matcher as M
+    lut = np.array([bin(i).count("1") for i in range(256)], np.int32)
+    errors = []
+
+    def work(seed):
+        rng = np.random.default_rng(seed)
+        try:
+            for it in range(40):
+                nq, nt = int(rng.integers(1, 400)), int(rng.integers(1, 900))
+                q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+                t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+                cnt = rng.integers(0, 12, nq)
+                off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+                idx = rng.integers(0, nt, int(off[-1])).astype(np.int32)
+                got = M.hamming_csr(q, t, off, idx)
+                qi = np.repeat(np.arange(nq), cnt)
+                want = lut[q[qi] ^ t[idx]].sum(1)
+                if not np.array_equal(got, want):
+                    errors.append(("csr", seed, it))
+                a, b = q[: min(nq, 50)], t[: min(nt, 70)]
+                if not np.array_equal(M.hamming_matrix(a, b), lut[a[:, None, :] ^ b[None, :, :]].sum(2)):
+                    errors.append(("matrix", seed, it))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("raised", seed, repr(e)))
+
+    ths = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_descriptor_distance_host_golden():
+    """The one-pair drop-in (liborbfe host popcount, no device call) against the reference's own
+    descriptor_distance outputs (ORBMatcher.py:12-14)."""
+    from pyorbslam_amd.matcher import ORBMatcher
+    z = np.load(GOLDEN / "matcher_distance.npz", allow_pickle=False)
+    m = ORBMatcher(0.8, True)
+    got = [m.descriptor_distance(z["a"][i], z["b"][i]) for i in range(len(z["a"]))]
+    assert got == z["dist"].tolist()
+    assert all(type(v) is int for v in got)
