@@ -50,6 +50,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc(const void* p, ui
                                              0x00020000);
 }
 
+// The same for a pointer that may differ between lanes (the compiler waterfalls the load over the
+// distinct resources).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc_lane(const void* p, uint32_t nbytes, uint32_t* bias) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    *bias = (uint32_t)a & 3u;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(a & ~(uint64_t)3), 0, nbytes + *bias, 0x00020000);
+}
+
 // Wave-wide sum (wave-uniform result): DPP quad_perm / row_ror sums inside each 16-lane row, then the
 // four row sums through v_readlane (no LDS-crossbar round trips).
 __device__ __forceinline__ int wave_sum(int v) {
@@ -1658,8 +1666,8 @@ __device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int 
     if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
         // the run lies inside one row of the level (the common case): 6 dword loads from the aligned
         // start, bounded to the level (reads past its end return 0), bytes re-aligned with v_alignbyte
-        uint32_t bias;
-        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * h), &bias);
+        uint32_t bias;  // lvl differs between the 16-lane groups of a wave (one keypoint and octave each)
+        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc_lane(lvl, (uint32_t)(stride * h), &bias);
         const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge)) + bias;
         const uint32_t sh = off & 3u, al = off - sh;
         uint32_t d[7];
