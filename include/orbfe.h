@@ -110,6 +110,28 @@ int orbfe_pyramid(orbfe_handle h, int32_t level, uint8_t* out, int32_t sheared, 
 int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, float* u_right, float* depth,
                        int8_t* status, int32_t* match_r, int32_t n_left);
 
+/* ---- per-frame stereo path (one Frame, one enqueue) ------------------------------------------
+ * Frame.__init__ (Frame.py:48-65) calls ExtractORB(0, left), ExtractORB(1, right) — two synchronous
+ * operator_kd calls, ORBextractor.cpp:1042-1104 — then GetImagePyramid on both extractors
+ * (orb_extractor.cpp:30) and compute_stereo_matches (Frame.py:161-279).  orbfe_frame_extract does all
+ * of it for one stereo pair in ONE enqueue on the handle's stream: both images copied in, the 2-image
+ * pipeline, the stereo match, optionally the sheared pyramids of both images (built on the device), and
+ * every result copied into page-locked host memory before a single synchronisation.  The fetch calls
+ * below then only copy host memory.  Both images are width x height u8 with row stride `stride`; an
+ * empty image (width or height 0) yields no keypoints (ORBextractor.cpp:1045-1046).  bf / fx as in
+ * orbfe_stereo_match. */
+int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* right, int32_t width, int32_t height,
+                        int32_t stride, double bf, float fx, int32_t want_pyramid);
+/* keypoints / descriptors of side 0 (left) or 1 (right) of the last frame (operator_kd's outputs) */
+int orbfe_frame_fetch(orbfe_handle h, int32_t side, orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out);
+/* stereo results of the last frame (layout and meaning as orbfe_stereo_match; *n_out = left count) */
+int orbfe_frame_fetch_stereo(orbfe_handle h, float* u_right, float* depth, int8_t* status, int32_t* match_r,
+                             int32_t cap, int32_t* n_out);
+/* GetImagePyramid()[level] of side 0 / 1 of the last frame: the reference's sheared view (see
+ * orbfe_pyramid).  Built at extraction when want_pyramid was set, otherwise now.  out = NULL queries
+ * the size. */
+int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* out, int32_t* w_out, int32_t* h_out);
+
 /* ---- device batch API (bench / batched-frames mode) ----------------------------------------
  * Images are device-resident, n_images x (height x img_pitch) u8, stereo pair p = images
  * (2p, 2p+1) = (left, right).  Results stay on device in handle-owned buffers. */

@@ -53,6 +53,12 @@ SIGNATURES = {
     "orbfe_pyramid": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
     "orbfe_stereo_match": [C.c_void_p, C.c_void_p, C.c_double, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_void_p, C.c_int32],
+    "orbfe_frame_extract": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_float,
+                            C.c_int32],
+    "orbfe_frame_fetch": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
+    "orbfe_frame_fetch_stereo": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                 C.POINTER(C.c_int32)],
+    "orbfe_frame_pyramid": [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
     "orbfe_batch_reserve": [C.c_void_p, C.c_int32, C.c_int32, C.c_int32],
     "orbfe_extract_batch_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p],
     "orbfe_stereo_batch_device": [C.c_void_p, C.c_int32, C.c_double, C.c_float, C.c_void_p],

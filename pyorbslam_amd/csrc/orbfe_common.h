@@ -46,6 +46,7 @@ struct LevelGeo {
     // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;
     // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
     int rs_ngrp, rs_nsrc, rs_sp;
+    int64_t shear_off;   // byte offset of the level's w x h sheared view inside an image's k_shear output
 };
 
 // One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.
@@ -83,6 +84,7 @@ struct Geo {
     int64_t ws_bytes;    // per-image pyramid workspace bytes (levels >= 1)
     int64_t blur_bytes;  // per-image blurred-pyramid bytes (all levels)
     int blur_tiles;      // k_blur tiles per image
+    int64_t shear_bytes; // per-image k_shear output (sum of w x h over levels)
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count
     int max_ncap;        // octree node capacity (max over levels of kp_cap)

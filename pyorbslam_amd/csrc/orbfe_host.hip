@@ -112,6 +112,14 @@ struct orbfe_ctx {
     double last_bf = 0.0;
     float last_fx = 0.f;
     bool have_single = false;          // orbfe_extract ran and its buffers are valid
+    // per-frame stereo path (orbfe_frame_extract): both images staged in d_in (pitch frame_pitch), the
+    // sheared pyramids in d_shear, every result copied into the pinned h_frame before one synchronisation
+    DevBuf<uint8_t> d_shear;
+    HostBuf<uint8_t> h_frame;
+    int64_t frame_pitch = 0;
+    bool have_frame = false, frame_pyr = false;
+    size_t fo_count = 0, fo_kps = 0, fo_desc = 0, fo_uR = 0, fo_depth = 0, fo_status = 0, fo_match = 0, fo_ovf = 0,
+           fo_shear = 0;
 
     ~orbfe_ctx() {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
@@ -242,7 +250,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.xt.clear();
     c.yt.clear();
     c.maxcell = 0;
-    int64_t ws = 0, bws = 0;
+    int64_t ws = 0, bws = 0, shear = 0;
     int kp_off = 0, key_off = 0, btile = 0;
     int64_t slot_off = 0;
     for (int l = 0; l < L; ++l) {
@@ -263,6 +271,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
             ws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
             resize_tables(g.lv[l - 1].w, g.lv[l - 1].h, Lg.w, Lg.h, c.prm.resize_simd_lanes, Lg, c.xt, c.yt);
         }
+        Lg.shear_off = shear;
+        shear += ((int64_t)Lg.w * Lg.h + 3) & ~(int64_t)3;
         Lg.blur_off = bws;
         bws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
         Lg.blur_tile0 = btile;
@@ -361,6 +371,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.ws_bytes = std::max<int64_t>(ws, 256);
     g.blur_bytes = bws;
     g.blur_tiles = btile;
+    g.shear_bytes = shear;
     g.slot_total = std::max<int64_t>(slot_off, 1);
     g.key_total = std::max(key_off, 1);
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
@@ -707,25 +718,147 @@ int orbfe_pyramid(orbfe_handle h, int32_t level, uint8_t* out, int32_t sheared, 
         if (w_out) *w_out = L.w;
         if (h_out) *h_out = L.h;
         if (!out) return;
-        std::vector<uint8_t> lv((size_t)L.w * L.h);
-        const uint8_t* src = level == 0 ? h->d_in.p : h->d_ws.p + L.ws_off;
-        const size_t spitch = level == 0 ? (size_t)L.w : (size_t)L.pitch;
-        HIPCK(hipMemcpy2D(lv.data(), L.w, src, spitch, L.w, L.h, hipMemcpyDeviceToHost));
         if (!sheared) {
-            std::memcpy(out, lv.data(), lv.size());
+            const uint8_t* src = level == 0 ? h->d_in.p : h->d_ws.p + L.ws_off;
+            const size_t spitch = level == 0 ? (size_t)L.w : (size_t)L.pitch;
+            HIPCK(hipMemcpy2D(out, L.w, src, spitch, L.w, L.h, hipMemcpyDeviceToHost));
             return;
         }
-        // ROI data pointer of the 19-px reflect-101 padded level read with stride w (caster ignores step)
-        const int pw = L.w + 2 * kEdge;
-        auto refl = [](int p, int n) {
-            p = p < 0 ? -p : p;
-            return p >= n ? 2 * n - 2 - p : p;
-        };
-        for (int64_t i = 0; i < (int64_t)L.w * L.h; ++i) {
-            const int64_t f = (int64_t)kEdge * pw + kEdge + i;
-            const int pr = (int)(f / pw), pc = (int)(f % pw);
-            out[i] = lv[(size_t)refl(pr - kEdge, L.h) * L.w + refl(pc - kEdge, L.w)];
+        // the reference caster's stride-ignoring view, built on the device (k_shear)
+        hipStream_t s = own(*h);
+        h->d_shear.ensure((size_t)h->geo.shear_bytes);
+        HIPCK(launch_shear(h->geo, h->d_in.p, (int64_t)h->W * h->H, h->d_ws.p, h->d_shear.p, 1, s));
+        HIPCK(hipMemcpyAsync(out, h->d_shear.p + L.shear_off, (size_t)L.w * L.h, hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+    });
+}
+
+int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* right, int32_t width, int32_t height,
+                        int32_t stride, double bf, float fx, int32_t want_pyramid) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        h->have_frame = h->frame_pyr = false;
+        h->have_single = false;
+        const bool empty = width <= 0 || height <= 0;  // operator_kd: _image.empty() -> return (:1045-1046)
+        if (!empty) {
+            if (!left || !right || stride < width) throw Error(ORBFE_EINVAL, "bad image pointer / stride");
+            reserve(*h, width, height, std::max(h->max_images, 2));
         }
+        const Geo& g = h->geo;
+        const size_t cap = empty ? 0 : (size_t)g.kp_cap;
+        size_t o = 0;
+        auto take = [&](size_t bytes) { const size_t r = o; o = (o + bytes + 255) & ~(size_t)255; return r; };
+        h->fo_ovf = take(sizeof(int));
+        h->fo_count = take(2 * sizeof(int));
+        h->fo_kps = take(2 * cap * sizeof(orbfe_keypoint));
+        h->fo_desc = take(2 * cap * 32);
+        h->fo_uR = take(cap * sizeof(float));
+        h->fo_depth = take(cap * sizeof(float));
+        h->fo_status = take(cap);
+        h->fo_match = take(cap * sizeof(int32_t));
+        h->fo_shear = take(empty ? 0 : 2 * (size_t)g.shear_bytes);
+        h->h_frame.ensure(o);
+        uint8_t* hb = h->h_frame.p;
+        if (empty) {
+            std::memset(hb + h->fo_count, 0, 2 * sizeof(int));
+            std::memset(hb + h->fo_ovf, 0, sizeof(int));
+            h->have_frame = true;
+            return;
+        }
+        hipStream_t s = own(*h);
+        const int64_t pitch = ((int64_t)width * height + 255) & ~(int64_t)255;
+        h->d_in.ensure(2 * (size_t)pitch);
+        HIPCK(hipMemcpy2DAsync(h->d_in.p, width, left, stride, width, height, hipMemcpyHostToDevice, s));
+        HIPCK(hipMemcpy2DAsync(h->d_in.p + pitch, width, right, stride, width, height, hipMemcpyHostToDevice, s));
+        HIPCK(hipMemsetAsync(h->d_overflow.p, 0, sizeof(int), s));
+        extract_range(*h, h->d_in.p, pitch, 0, 2, s, false, false);
+        stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, s);
+        if (want_pyramid) {
+            h->d_shear.ensure(2 * (size_t)g.shear_bytes);
+            HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, s));
+        }
+        auto d2h = [&](size_t off, const void* src, size_t bytes) {
+            HIPCK(hipMemcpyAsync(hb + off, src, bytes, hipMemcpyDeviceToHost, s));
+        };
+        d2h(h->fo_ovf, h->d_overflow.p, sizeof(int));
+        d2h(h->fo_count, h->d_count.p, 2 * sizeof(int));
+        d2h(h->fo_kps, h->d_kps.p, 2 * cap * sizeof(orbfe_keypoint));
+        d2h(h->fo_desc, h->d_desc.p, 2 * cap * 32);
+        d2h(h->fo_uR, h->d_uR.p, cap * sizeof(float));
+        d2h(h->fo_depth, h->d_depth.p, cap * sizeof(float));
+        d2h(h->fo_status, h->d_status.p, cap);
+        d2h(h->fo_match, h->d_match.p, cap * sizeof(int32_t));
+        if (want_pyramid) d2h(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
+        HIPCK(hipStreamSynchronize(s));
+        h->last_in = h->d_in.p;
+        h->last_pitch = h->frame_pitch = pitch;
+        h->last_images = 2;
+        h->last_pairs = 1;
+        h->last_stream = s;
+        h->last_bf = bf;
+        h->last_fx = fx;
+        int ovf = 0;
+        std::memcpy(&ovf, hb + h->fo_ovf, sizeof(int));
+        if (ovf) throw Error(ORBFE_EOVERFLOW, "on-device capacity bound exceeded (code " + std::to_string(ovf) + ")");
+        h->have_frame = true;
+        h->frame_pyr = want_pyramid != 0;
+    });
+}
+
+int orbfe_frame_fetch(orbfe_handle h, int32_t side, orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (!h->have_frame) throw Error(ORBFE_ESTATE, "no frame extracted with orbfe_frame_extract");
+        if (side != 0 && side != 1) throw Error(ORBFE_EINVAL, "side must be 0 (left) or 1 (right)");
+        const uint8_t* hb = h->h_frame.p;
+        int n = 0;
+        std::memcpy(&n, hb + h->fo_count + side * sizeof(int), sizeof(int));
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "keypoint buffer too small");
+        const size_t kc = (size_t)h->geo.kp_cap;
+        if (n && kps) std::memcpy(kps, hb + h->fo_kps + side * kc * sizeof(orbfe_keypoint), n * sizeof(orbfe_keypoint));
+        if (n && desc) std::memcpy(desc, hb + h->fo_desc + side * kc * 32, (size_t)n * 32);
+    });
+}
+
+int orbfe_frame_fetch_stereo(orbfe_handle h, float* u_right, float* depth, int8_t* status, int32_t* match_r,
+                             int32_t cap, int32_t* n_out) {
+    return guarded([&] {
+        if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
+        if (!h->have_frame) throw Error(ORBFE_ESTATE, "no frame extracted with orbfe_frame_extract");
+        const uint8_t* hb = h->h_frame.p;
+        int n = 0;
+        std::memcpy(&n, hb + h->fo_count, sizeof(int));
+        *n_out = n;
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "buffer too small");
+        if (n && u_right) std::memcpy(u_right, hb + h->fo_uR, n * sizeof(float));
+        if (n && depth) std::memcpy(depth, hb + h->fo_depth, n * sizeof(float));
+        if (n && status) std::memcpy(status, hb + h->fo_status, n);
+        if (n && match_r) std::memcpy(match_r, hb + h->fo_match, n * sizeof(int32_t));
+    });
+}
+
+int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* out, int32_t* w_out, int32_t* h_out) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (!h->have_frame || h->W <= 0 || h->last_images != 2) throw Error(ORBFE_ESTATE, "no frame extracted");
+        if (side != 0 && side != 1) throw Error(ORBFE_EINVAL, "side must be 0 (left) or 1 (right)");
+        if (level < 0 || level >= h->geo.nlevels) throw Error(ORBFE_EINVAL, "level out of range");
+        const Geo& g = h->geo;
+        const LevelGeo& L = g.lv[level];
+        if (w_out) *w_out = L.w;
+        if (h_out) *h_out = L.h;
+        if (!out) return;
+        if (!h->frame_pyr) {  // not requested at extraction: build and fetch both views now
+            hipStream_t s = own(*h);
+            h->d_shear.ensure(2 * (size_t)g.shear_bytes);
+            HIPCK(launch_shear(g, h->d_in.p, h->frame_pitch, h->d_ws.p, h->d_shear.p, 2, s));
+            HIPCK(hipMemcpyAsync(h->h_frame.p + h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes,
+                                 hipMemcpyDeviceToHost, s));
+            HIPCK(hipStreamSynchronize(s));
+            h->frame_pyr = true;
+        }
+        std::memcpy(out, h->h_frame.p + h->fo_shear + side * (size_t)g.shear_bytes + L.shear_off, (size_t)L.w * L.h);
     });
 }
 

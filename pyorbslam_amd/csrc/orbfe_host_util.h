@@ -66,4 +66,29 @@ struct DevBuf {
     }
 };
 
+// Page-locked host buffer (hipHostMalloc): the per-frame results come back with asynchronous copies
+// into it and one stream synchronisation.
+template <class T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~HostBuf() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void ensure(size_t count) {
+        if (count <= n && p) return;
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipHostMalloc((void**)&p, count * sizeof(T), hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw Error(ORBFE_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        }
+        n = count;
+    }
+};
+
 }  // namespace orbfe

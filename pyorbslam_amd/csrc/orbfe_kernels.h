@@ -55,6 +55,9 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
                            const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
                            int* out_count, const uint32_t* mw, int n_images, hipStream_t s, int variant = 0);
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s);
+// sheared views of every level (GetImagePyramid), out: n_images x g.shear_bytes
+hipError_t launch_shear(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* out, int n_images,
+                        hipStream_t s);
 hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int* out, hipStream_t s);
 hipError_t launch_hamming_search(const uint8_t* q, int nq, const uint8_t* tr, const int* off, const int* idx, int* bd,
                                  int* bi, int* sd, int* si, int* all_d, hipStream_t s);

@@ -1594,6 +1594,36 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
     }
 }
 
+// ------------------------------------------------------------------------------- k_shear
+// GetImagePyramid as the reference returns it (orb_extractor.cpp:30): the Mat -> ndarray caster ignores
+// Mat::step (opencv_type_casters.h:232-239), so row r of level l's (h, w) array is bytes
+// [19 (w + 38) + 19 + r w, + w) of the 19-px reflect-101 padded level buffer (ORBextractor.cpp:1112-1128).
+// One thread per 4 output bytes of all levels of an image (dword stores; a level's tail bytes singly;
+// every level's region starts 4-byte aligned).
+__global__ __launch_bounds__(256) void k_shear(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                               const uint8_t* __restrict__ ws, uint8_t* __restrict__ out) {
+    const int img = blockIdx.y;
+    const int64_t i0 = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (i0 >= g.shear_bytes) return;
+    int l = 0;
+    while (l + 1 < g.nlevels && i0 >= g.lv[l + 1].shear_off) ++l;
+    const LevelGeo& L = g.lv[l];
+    int stride;
+    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
+    const int pw = L.w + 2 * kEdge;
+    const int64_t i = i0 - L.shear_off, n = (int64_t)L.w * L.h;
+    uint8_t* o = out + (int64_t)img * g.shear_bytes + i0;
+    uint32_t v = 0;
+    for (int b = 0; b < 4 && i + b < n; ++b) {
+        const int64_t f = (int64_t)kEdge * pw + kEdge + i + b;
+        const int pr = (int)(f / pw), pc = (int)(f - (int64_t)pr * pw);
+        const uint8_t px = lvl[(int64_t)reflect101(pr - kEdge, L.h) * stride + reflect101(pc - kEdge, L.w)];
+        v |= (uint32_t)px << (8 * b);
+        if (i + 4 > n) o[b] = px;  // the level's last bytes (its region is padded to 4 bytes)
+    }
+    if (i + 4 <= n) *(uint32_t*)o = v;  // levels start at 4-byte aligned offsets (host: shear_off)
+}
+
 // ------------------------------------------------------------------------------- k_stereo
 __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Python round(): half to even
 
@@ -2028,6 +2058,14 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
     hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);
     hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 15) / 16, n_pairs), dim3(256), 0, s, g, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shear(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* out, int n_images,
+                        hipStream_t s) {
+    if (n_images <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_shear, dim3((unsigned)((g.shear_bytes + 1023) / 1024), n_images), dim3(256), 0, s, g, in, in_pitch,
+                       ws, out);
     return hipGetLastError();
 }
 

@@ -11,16 +11,17 @@ the host, with the reference's element types:
     zero disparity  Python float: uR = uL - 0.01, depth = mbf / 0.01 (Frame.py:273-277)
 
 Use either as a function, `compute_stereo_matches(frame)`, or patch the reference class once:
-`install(Frame)`.
+`install(Frame)` (also batches Frame.ExtractORB's two images into one enqueue and replaces Frame.copy).
 """
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
 from ._lib import call, ptr
-from .pyORBExtractor import ORBextractor
+from .pyORBExtractor import ORBextractor, keypoint_tuples
 
 
 def stereo_match_arrays(left: ORBextractor, right: ORBextractor, mbf: float, fx32) -> dict:
@@ -36,29 +37,74 @@ def stereo_match_arrays(left: ORBextractor, right: ORBextractor, mbf: float, fx3
 
 
 def to_reference_lists(res: dict, kps_left: np.ndarray, mbf: float) -> tuple[list, list]:
-    uR, dep = [], []
-    xs = kps_left["x"].tolist() if len(kps_left) else []
-    for i, s in enumerate(res["status"].tolist()):
-        if s == 0:
-            uR.append(-1)
-            dep.append(-1)
-        elif s == 1:
-            uR.append(np.float32(res["u_right"][i]))
-            dep.append(np.float32(res["depth"][i]))
-        else:
-            uR.append(xs[i] - 0.01)
-            dep.append(mbf / 0.01)
+    st = res["status"]
+    uR = list(res["u_right"])  # np.float32 scalars, as the reference's NumPy-2 float32 chain leaves them
+    dep = list(res["depth"])
+    for i in np.flatnonzero(st == 0).tolist():
+        uR[i] = -1
+        dep[i] = -1
+    zero = np.flatnonzero(st == 2).tolist()
+    if zero:
+        xs = kps_left["x"]
+        for i in zero:  # disparity <= 0 -> 0.01 in Python double precision (Frame.py:273-277)
+            uR[i] = float(xs[i]) - 0.01
+            dep[i] = mbf / 0.01
     return uR, dep
 
 
 def compute_stereo_matches(frame) -> None:
+    """Frame.compute_stereo_matches (Frame.py:161-279).  After the pair-batched ExtractORB below the
+    result is already on the host (computed in the same enqueue as the extraction); otherwise the two
+    extractors' last single-image extractions are matched on the GPU now."""
     left, right = frame.mpORBextractorLeft, frame.mpORBextractorRight
     if not isinstance(left, ORBextractor) or not isinstance(right, ORBextractor):
         raise TypeError("compute_stereo_matches needs pyorbslam_amd.pyORBExtractor.ORBextractor extractors")
     if len(left.last_keypoints) != frame.N:
         raise RuntimeError("Frame.N does not match the left extractor's last extraction")
-    res = stereo_match_arrays(left, right, frame.mbf, frame.mK[0][0])
+    res = left.stereo_result
+    if res is None or getattr(left, "_stereo_partner", None) is not right:
+        res = stereo_match_arrays(left, right, frame.mbf, frame.mK[0][0])
     frame.mvuRight, frame.mvDepth = to_reference_lists(res, left.last_keypoints, frame.mbf)
+
+
+def _keypoint_cls(frame):
+    """cv2.KeyPoint as the Frame class's module sees it (Frame.py:6, 117, 121); subclasses defined
+    elsewhere resolve through their bases."""
+    for cls in type(frame).__mro__:
+        cv2 = getattr(sys.modules.get(cls.__module__), "cv2", None)
+        if cv2 is not None and hasattr(cv2, "KeyPoint"):
+            return cv2.KeyPoint
+    raise RuntimeError(f"no cv2.KeyPoint in the modules of {type(frame).__name__} or its bases")
+
+
+def extract_orb(self, flag, image) -> None:
+    """Frame.ExtractORB (Frame.py:114-121) with the stereo pair in ONE enqueue.
+
+    Frame.__init__ sets mleft / mright, mbf and mK before ExtractORB(0, mleft) (Frame.py:33-49), so the
+    left call extracts both images, matches them and builds both sheared pyramids on the GPU
+    (ORBextractor.operator_kd_stereo); ExtractORB(1, mright) then takes the waiting right results,
+    GetImagePyramid() returns the device-built views and compute_stereo_matches the matched arrays.  The
+    attributes written are the reference's: mvKeys_ / mDescriptors / mvKeys (flag 0) and mvKeysRight_ /
+    mDescriptorsRight / mvKeysRight (flag 1).  Any other call sequence extracts one image, like the
+    reference."""
+    left, right = self.mpORBextractorLeft, self.mpORBextractorRight
+    KeyPoint = _keypoint_cls(self)
+    if flag == 0:
+        mright = getattr(self, "mright", None)
+        if (image is getattr(self, "mleft", None) and mright is not None and isinstance(left, ORBextractor)
+                and isinstance(right, ORBextractor) and right is not left):
+            kl, dl, _, _ = left.operator_kd_stereo(image, mright, right, self.mbf, self.mK[0][0])
+            self.mvKeys_, self.mDescriptors = keypoint_tuples(kl), dl
+        else:
+            self.mvKeys_, self.mDescriptors = left.operator_kd(image)
+        self.mvKeys = [KeyPoint(*kp) for kp in self.mvKeys_]
+    elif flag == 1:
+        pend = right.take_pending(image) if isinstance(right, ORBextractor) else None
+        if pend is not None:
+            self.mvKeysRight_, self.mDescriptorsRight = keypoint_tuples(pend[0]), pend[1]
+        else:
+            self.mvKeysRight_, self.mDescriptorsRight = right.operator_kd(image)
+        self.mvKeysRight = [KeyPoint(*kp) for kp in self.mvKeysRight_]
 
 
 # Frame.__init__'s attributes that come straight from its arguments (Frame.py:15-44), which Frame.copy
@@ -127,9 +173,12 @@ def frame_copy(self, frame):
     return new
 
 
-def install(frame_cls, copy: bool = True) -> None:
-    """Replace Frame.compute_stereo_matches (Frame.py:161) and, unless copy=False, Frame.copy
-    (Frame.py:75) of the reference class in place."""
+def install(frame_cls, copy: bool = True, pair: bool = True) -> None:
+    """Replace Frame.compute_stereo_matches (Frame.py:161), unless pair=False Frame.ExtractORB
+    (Frame.py:114: both images in one enqueue) and unless copy=False Frame.copy (Frame.py:75) of the
+    reference class in place."""
     frame_cls.compute_stereo_matches = compute_stereo_matches
+    if pair:
+        frame_cls.ExtractORB = extract_orb
     if copy:
         frame_cls.copy = frame_copy

@@ -35,6 +35,11 @@ class ORBextractor:
         self._kps = np.zeros(0, KP_DTYPE)
         self._desc = np.zeros((0, 32), np.uint8)
         self._extracted = False
+        # after operator_kd_stereo: (handle, side) whose frame holds this extractor's pyramid, the stereo
+        # result of the pair (left extractor), and the right image whose results wait for ExtractORB(1)
+        self._pyr_src = None
+        self.stereo_result = None
+        self._pending_image = None
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -76,45 +81,99 @@ class ORBextractor:
         out = []
         for l in range(self._nlevels):
             w, h = C.c_int32(), C.c_int32()
-            call("orbfe_pyramid", self._h, l, None, int(sheared), C.byref(w), C.byref(h))
-            a = np.empty((h.value, w.value), np.uint8)
-            call("orbfe_pyramid", self._h, l, ptr(a), int(sheared), C.byref(w), C.byref(h))
+            if self._pyr_src is not None and sheared:
+                src, side = self._pyr_src
+                call("orbfe_frame_pyramid", src, side, l, None, C.byref(w), C.byref(h))
+                a = np.empty((h.value, w.value), np.uint8)
+                call("orbfe_frame_pyramid", src, side, l, ptr(a), C.byref(w), C.byref(h))
+            else:
+                if self._pyr_src is not None:
+                    raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
+                call("orbfe_pyramid", self._h, l, None, int(sheared), C.byref(w), C.byref(h))
+                a = np.empty((h.value, w.value), np.uint8)
+                call("orbfe_pyramid", self._h, l, ptr(a), int(sheared), C.byref(w), C.byref(h))
             out.append(a)
         return out
 
     # ---- operator_kd (orb_extractor.cpp:31-38, ORBextractor.cpp:1042-1104) -----------------------------
     def operator_kd(self, image):
         kps, desc = self.extract(image)
-        tuples = [(float(k[0]), float(k[1]), float(k[2]), float(k[3]), float(k[4]), int(k[5])) for k in kps.tolist()]
-        return tuples, desc
+        return keypoint_tuples(kps), desc
 
-    def extract(self, image) -> tuple[np.ndarray, np.ndarray]:
-        """operator_kd with structured-array output (no per-keypoint Python objects)."""
-        img = np.asarray(image)
-        if img.ndim not in (2, 3):
-            raise RuntimeError(f"Unsupported dim {img.ndim}, only support 2d, or 3-d")
-        if img.dtype != np.uint8:
-            # the reference casts int32/float32 to CV_32S/CV_32F (undefined downstream) and rejects the rest
-            raise RuntimeError("Unsupported type, only support uchar, int32, float")
-        if img.ndim == 3:
-            if img.shape[2] != 1:
-                raise RuntimeError("multi-channel images are undefined behaviour in the reference (CV_8UC1 assert "
-                                   "compiled out); pass a grayscale image")
-            img = img[:, :, 0]
-        img = np.ascontiguousarray(img)
-        h, w = img.shape
-        cap = int(self._params.nfeatures) + 8 * self._nlevels + 64
-        kps = np.empty(cap, KP_DTYPE)
-        desc = np.empty((cap, 32), np.uint8)
-        n = C.c_int32()
-        call("orbfe_extract", self._h, ptr(img), w, h, w, ptr(kps), ptr(desc), cap, C.byref(n))
-        self._extracted = w > 0 and h > 0
-        n = n.value
+    def _cap(self) -> int:
+        return int(self._params.nfeatures) + 8 * self._nlevels + 64
+
+    def _set_result(self, kps: np.ndarray, desc: np.ndarray, n: int, extracted: bool) -> None:
+        self._extracted = extracted
         if n == 0:
             # _descriptors.release() / never created -> empty cv::Mat -> (0, 0) array
             self._kps, self._desc = kps[:0].copy(), np.zeros((0, 0), np.uint8)
         else:
             self._kps, self._desc = kps[:n].copy(), desc[:n].copy()
+
+    def extract(self, image) -> tuple[np.ndarray, np.ndarray]:
+        """operator_kd with structured-array output (no per-keypoint Python objects)."""
+        img = as_gray_u8(image)
+        h, w = img.shape
+        cap = self._cap()
+        kps = np.empty(cap, KP_DTYPE)
+        desc = np.empty((cap, 32), np.uint8)
+        n = C.c_int32()
+        self._pyr_src = None
+        self.stereo_result = None
+        self._pending_image = None
+        call("orbfe_extract", self._h, ptr(img), w, h, w, ptr(kps), ptr(desc), cap, C.byref(n))
+        self._set_result(kps, desc, n.value, w > 0 and h > 0)
+        return self._kps, self._desc
+
+    # ---- one stereo frame in one enqueue ---------------------------------------------------------------
+    def operator_kd_stereo(self, left, right, right_extractor: "ORBextractor", mbf: float, fx32,
+                           want_pyramid: bool = True):
+        """Frame.__init__'s ExtractORB(0, left) + ExtractORB(1, right) + GetImagePyramid() of both
+        extractors + compute_stereo_matches (Frame.py:48-65, 161-279) as ONE enqueue on this extractor's
+        handle (orbfe_frame_extract): one host->device copy per image, the 2-image pipeline, the stereo
+        match and the sheared pyramids, then one synchronisation.
+
+        Afterwards this extractor holds the left results and `right_extractor` the right ones, exactly as
+        if each had run operator_kd (last_keypoints, last_descriptors, GetImagePyramid), and
+        self.stereo_result holds the raw stereo arrays of the pair.  Returns
+        (kps_left, desc_left, kps_right, desc_right) as structured arrays."""
+        if right_extractor is self:
+            raise ValueError("the right image needs its own extractor (the reference keeps one per camera)")
+        L, R = as_gray_u8(left), as_gray_u8(right)
+        if L.shape != R.shape:
+            raise RuntimeError("left and right images differ in size")
+        h, w = L.shape
+        call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
+             int(bool(want_pyramid)))
+        cap = self._cap()
+        out = []
+        for side, ex in ((0, self), (1, right_extractor)):
+            kps = np.empty(cap, KP_DTYPE)
+            desc = np.empty((cap, 32), np.uint8)
+            n = C.c_int32()
+            call("orbfe_frame_fetch", self._h, side, ptr(kps), ptr(desc), cap, C.byref(n))
+            ex._set_result(kps, desc, n.value, w > 0 and h > 0)
+            ex._pyr_src = (self._h, side) if w > 0 and h > 0 else None
+            ex.stereo_result = None
+            out += [ex._kps, ex._desc]
+        n = len(self._kps)
+        res = dict(u_right=np.empty(n, np.float32), depth=np.empty(n, np.float32), status=np.empty(n, np.int8),
+                   match_r=np.empty(n, np.int32))
+        nn = C.c_int32()
+        call("orbfe_frame_fetch_stereo", self._h, ptr(res["u_right"]), ptr(res["depth"]), ptr(res["status"]),
+             ptr(res["match_r"]), n, C.byref(nn))
+        self.stereo_result = res
+        self._stereo_partner = right_extractor
+        right_extractor._pending_image = right
+        return tuple(out)
+
+    def take_pending(self, image):
+        """The right-image results of the last operator_kd_stereo if `image` is that call's right image
+        (Frame.ExtractORB(1, ...) right after ExtractORB(0, ...)); None otherwise."""
+        if self._pending_image is None or self._pending_image is not image:
+            return None
+        self._pending_image = None
         return self._kps, self._desc
 
     @property
@@ -124,3 +183,26 @@ class ORBextractor:
     @property
     def last_descriptors(self) -> np.ndarray:
         return self._desc
+
+
+def as_gray_u8(image) -> np.ndarray:
+    """The reference caster's input rules (opencv_type_casters.h:184-200): 2-D uint8, or 3-D with one
+    channel; int32 / float32 are undefined behaviour downstream and every other dtype raises."""
+    img = np.asarray(image)
+    if img.ndim not in (2, 3):
+        raise RuntimeError(f"Unsupported dim {img.ndim}, only support 2d, or 3-d")
+    if img.dtype != np.uint8:
+        # the reference casts int32/float32 to CV_32S/CV_32F (undefined downstream) and rejects the rest
+        raise RuntimeError("Unsupported type, only support uchar, int32, float")
+    if img.ndim == 3:
+        if img.shape[2] != 1:
+            raise RuntimeError("multi-channel images are undefined behaviour in the reference (CV_8UC1 assert "
+                               "compiled out); pass a grayscale image")
+        img = img[:, :, 0]
+    return np.ascontiguousarray(img)
+
+
+def keypoint_tuples(kps: np.ndarray) -> list:
+    """cv::KeyPoint tuples (x, y, size, angle, response, octave) as the reference caster builds them
+    (opencv_type_casters.h:106-108): Python floats (exact f32 values) and an int."""
+    return kps.tolist()

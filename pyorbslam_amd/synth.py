@@ -78,3 +78,104 @@ def shifted_right(left: np.ndarray, seed: int, dmax: int = 48, block: int = 16) 
         right[r0:r1] = pad[r0:r1, int(disp[b]):int(disp[b]) + w]
     right += rng.integers(-2, 3, size=right.shape).astype(np.float32)
     return np.ascontiguousarray(np.clip(np.rint(right), 0, 255).astype(np.uint8))
+
+
+# ------------------------------------------------------------------------------ moving stereo sequence
+KITTI_CAM = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448)  # KITTI00-02.yaml:7-10, 37
+
+
+def _texture(rng: np.random.Generator, h: int, w: int, rmax: int = 60, amp: float = 1.0) -> np.ndarray:
+    t = np.full((h, w), 128.0 - 70.0 * amp, np.float32)
+    for cell, a in ((40, 90.0), (10, 50.0), (3, 22.0)):
+        t += _value_noise(rng, h, w, cell, a * amp)
+    for _ in range(max(6, (h * w) // 2500)):
+        rw, rh = rng.integers(3, min(rmax, w - 1)), rng.integers(3, min(rmax, h - 1))
+        x0, y0 = rng.integers(0, w - rw), rng.integers(0, h - rh)
+        t[y0:y0 + rh, x0:x0 + rw] += rng.uniform(-60.0, 60.0) * amp
+    return t
+
+
+class StereoSequence:
+    """A rectified stereo camera moving through a scene of textured fronto-parallel planes, rendered
+    deterministically (float64 ray casting, bilinear texture lookup, +-2 sensor noise per image).
+
+    Used as the synthetic stand-in for KITTI-00 (BASELINE config C3): the camera moves
+    forward (speed m/frame) with a lateral / vertical sway and a small yaw / pitch oscillation, so
+    consecutive frames share most features at changing scales and the constant-velocity prediction of
+    Tracking.track_with_motion_model (Tracking.py:583) is close to, but not equal to, the true pose.
+    pose(k) is the ground-truth Tcw (float32 4x4, world -> camera); frame(k) the (left, right) images."""
+
+    def __init__(self, seed: int = 0, width: int = KITTI_WH[0], height: int = KITTI_WH[1], speed: float = 0.6,
+                 cam: dict | None = None, n_boxes: int = 40):
+        self.seed, self.width, self.height, self.speed = int(seed), int(width), int(height), float(speed)
+        self.cam = dict(KITTI_CAM if cam is None else cam)
+        self.baseline = self.cam["bf"] / self.cam["fx"]
+        rng = np.random.Generator(np.random.PCG64(1_000_003 + self.seed))
+        # (z, x0, x1, y0, y1, texel size, texture); the background plane last
+        self.layers = []
+        for _ in range(n_boxes):
+            z = float(rng.uniform(40.0, 160.0))
+            half = 0.9 * z  # the field of view is about +-0.85 z wide and +-0.26 z high
+            sx, sy = float(rng.uniform(0.06, 0.3)) * z, float(rng.uniform(0.04, 0.16)) * z
+            x0, y0 = float(rng.uniform(-half, half - sx)), float(rng.uniform(-0.3 * z, 0.3 * z - sy))
+            texel = float(rng.uniform(0.0006, 0.0016)) * z
+            th, tw = int(sy / texel) + 2, int(sx / texel) + 2
+            self.layers.append((z, x0, x0 + sx, y0, y0 + sy, texel, _texture(rng, th, tw)))
+        self.layers.sort(key=lambda a: a[0])
+        bg_texel = 0.5
+        self.layers.append((240.0, -420.0, 420.0, -150.0, 150.0, bg_texel,
+                            _texture(rng, int(300 / bg_texel) + 2, int(840 / bg_texel) + 2, rmax=24, amp=0.6)))
+
+    def _rwc_center(self, k: int) -> tuple[np.ndarray, np.ndarray]:
+        yaw, pitch = 0.03 * np.sin(0.09 * k), 0.012 * np.sin(0.13 * k + 0.5)
+        cy, sy, cp, sp = np.cos(yaw), np.sin(yaw), np.cos(pitch), np.sin(pitch)
+        ry = np.array([[cy, 0.0, sy], [0.0, 1.0, 0.0], [-sy, 0.0, cy]])
+        rx = np.array([[1.0, 0.0, 0.0], [0.0, cp, -sp], [0.0, sp, cp]])
+        c = np.array([2.0 * np.sin(0.07 * k), 0.3 * np.sin(0.11 * k), self.speed * k])
+        return ry @ rx, c
+
+    def pose(self, k: int) -> np.ndarray:
+        rwc, c = self._rwc_center(k)
+        t = np.eye(4, dtype=np.float32)
+        t[:3, :3] = rwc.T.astype(np.float32)
+        t[:3, 3] = (-rwc.T @ c).astype(np.float32)
+        return t
+
+    def _render(self, rwc: np.ndarray, c: np.ndarray, noise_seed: int) -> np.ndarray:
+        h, w, cam = self.height, self.width, self.cam
+        u = (np.arange(w, dtype=np.float64) - cam["cx"]) / cam["fx"]
+        v = (np.arange(h, dtype=np.float64) - cam["cy"]) / cam["fy"]
+        dc = np.stack(np.broadcast_arrays(u[None, :], v[:, None], np.ones((1, 1))), -1)  # (h, w, 3)
+        dw = dc @ rwc.T
+        best_t = np.full((h, w), np.inf)
+        best_l = np.full((h, w), -1, np.int32)
+        for li, (z, x0, x1, y0, y1, _, _) in enumerate(self.layers):
+            t = (z - c[2]) / dw[..., 2]
+            px, py = c[0] + t * dw[..., 0], c[1] + t * dw[..., 1]
+            hit = (t > 0) & (t < best_t) & (px >= x0) & (px < x1) & (py >= y0) & (py < y1)
+            best_t[hit] = t[hit]
+            best_l[hit] = li
+        img = np.full((h, w), 20.0, np.float64)
+        for li, (z, x0, x1, y0, y1, texel, tex) in enumerate(self.layers):
+            m = best_l == li
+            if not m.any():
+                continue
+            t = best_t[m]
+            tx = (c[0] + t * dw[..., 0][m] - x0) / texel
+            ty = (c[1] + t * dw[..., 1][m] - y0) / texel
+            ix, iy = np.floor(tx).astype(np.int64), np.floor(ty).astype(np.int64)
+            fx, fy = tx - ix, ty - iy
+            ix = np.clip(ix, 0, tex.shape[1] - 2)
+            iy = np.clip(iy, 0, tex.shape[0] - 2)
+            a, b = tex[iy, ix].astype(np.float64), tex[iy, ix + 1].astype(np.float64)
+            cc, d = tex[iy + 1, ix].astype(np.float64), tex[iy + 1, ix + 1].astype(np.float64)
+            img[m] = (a * (1 - fx) + b * fx) * (1 - fy) + (cc * (1 - fx) + d * fx) * fy
+        rng = np.random.Generator(np.random.PCG64(noise_seed))
+        img += rng.integers(-2, 3, size=img.shape)
+        return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
+
+    def frame(self, k: int) -> tuple[np.ndarray, np.ndarray]:
+        rwc, c = self._rwc_center(k)
+        left = self._render(rwc, c, 7_000_000 + 1000 * self.seed + 2 * k)
+        right = self._render(rwc, c + rwc @ np.array([self.baseline, 0.0, 0.0]), 7_000_000 + 1000 * self.seed + 2 * k + 1)
+        return left, right

@@ -187,3 +187,40 @@ def test_batch_path_misaligned_images(wh):
         batch = fe.fetch_stereo(p)
         for k in ("status", "u_right", "depth", "match_r"):
             assert np.array_equal(single[k], batch[k]), (p, k)
+
+
+def test_pair_path_equals_single_path_and_oracle_pyramids():
+    """operator_kd_stereo (one enqueue per frame, orbfe_frame_extract) against two operator_kd calls plus
+    orbfe_stereo_match, and its device-built sheared pyramids against the oracle's (GetImagePyramid,
+    orb_extractor.cpp:30)."""
+    from oracle.oracle import OracleExtractor
+    for seed, (w, h), prm in ((5, (1241, 376), KITTI), (6, (641, 333), dict(KITTI, nfeatures=700))):
+        L, R = synth.make_pair(seed, w, h)
+        a, b = ORBextractor(**prm), ORBextractor(**prm)
+        kl, dl, kr, dr = a.operator_kd_stereo(L, R, b, BF, np.float32(FX))
+        sL, sR = ORBextractor(**prm), ORBextractor(**prm)
+        skl, sdl = sL.extract(L)
+        skr, sdr = sR.extract(R)
+        assert kl.tobytes() == skl.tobytes() and np.array_equal(dl, sdl)
+        assert kr.tobytes() == skr.tobytes() and np.array_equal(dr, sdr)
+        assert b.last_keypoints.tobytes() == skr.tobytes()
+        single = F.stereo_match_arrays(sL, sR, BF, np.float32(FX))
+        for k in ("status", "u_right", "depth", "match_r"):
+            assert np.array_equal(single[k], a.stereo_result[k]), k
+        for ex, img in ((a, L), (b, R)):
+            o = OracleExtractor(**prm)
+            o.extract(img)
+            got, want = ex.GetImagePyramid(), o.sheared_pyramid()
+            assert len(got) == len(want)
+            for g_, w_ in zip(got, want):
+                assert g_.shape == w_.shape and np.array_equal(g_, w_)
+        # the right extractor's results wait for ExtractORB(1, R) exactly once
+        assert b.take_pending(R) is not None and b.take_pending(R) is None
+
+
+def test_pair_path_empty_image():
+    a, b = ORBextractor(**KITTI), ORBextractor(**KITTI)
+    e = np.zeros((0, 0), np.uint8)
+    kl, dl, kr, dr = a.operator_kd_stereo(e, e, b, BF, np.float32(FX))
+    assert len(kl) == 0 and dl.shape == (0, 0) and len(kr) == 0 and dr.shape == (0, 0)
+    assert len(a.stereo_result["status"]) == 0
