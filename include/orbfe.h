@@ -181,6 +181,21 @@ typedef struct orbfe_batch_view {
 } orbfe_batch_view;
 int orbfe_batch_view_get(orbfe_handle h, orbfe_batch_view* view);
 
+/* Synchronise the handle's last stream and read the overflow word of the last batch (0 = every
+ * on-device capacity bound held; otherwise the OR of the codes of the bounds that were hit). */
+int orbfe_batch_status(orbfe_handle h, int32_t* overflow);
+
+/* Batched-frames mode, multi-GPU: every pair's results as one fixed-capacity byte record, packed on the
+ * device for the rank-0 gather (north star: "RCCL over xGMI only for the trivial gather of per-frame
+ * keypoints").  Record layout (pyorbslam_amd/dist.py): counts L, R (2 x i32) | keypoints L, R
+ * (kp_cap x orbfe_keypoint each) | descriptors L, R (kp_cap x 32 B each) | u_right, depth (kp_cap x f32)
+ * | status (kp_cap x i8), padded to 16 bytes: orbfe_batch_record_bytes.  orbfe_batch_pack_device writes
+ * pairs [pair0, pair0 + n_pairs) of the last stereo batch to d_records (n_pairs x rec_bytes, 4-byte
+ * aligned) on hip_stream, without synchronising. */
+int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes);
+int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0, int32_t n_pairs,
+                            void* hip_stream);
+
 /* Copy the results of image `image` (and of pair image/2 when image is even and a stereo
  * batch ran) of the last batch to host buffers.  Synchronises the handle's last stream. */
 int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap,

@@ -64,6 +64,12 @@ class StereoFrontEnd:
         call("orbfe_extract_batch_device", self._h, C.c_void_p(images.data_ptr()), self.width * self.height, n,
              C.c_void_p(stream_ptr))
 
+    def overflow(self) -> int:
+        """Overflow word of the last batch (0 = no on-device capacity bound was hit); synchronises."""
+        v = C.c_int32()
+        call("orbfe_batch_status", self._h, C.byref(v))
+        return v.value
+
     def fetch_image(self, i: int) -> tuple[np.ndarray, np.ndarray]:
         kps = np.empty(self.kp_cap, KP_DTYPE)
         desc = np.empty((self.kp_cap, 32), np.uint8)

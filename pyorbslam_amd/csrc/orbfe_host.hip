@@ -962,6 +962,44 @@ int orbfe_batch_view_get(orbfe_handle h, orbfe_batch_view* v) {
     });
 }
 
+int orbfe_batch_status(orbfe_handle h, int32_t* overflow) {
+    return guarded([&] {
+        if (!h || !overflow) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->last_stream) HIPCK(hipStreamSynchronize(h->last_stream));
+        int ovf = 0;
+        if (h->d_overflow.p) HIPCK(hipMemcpy(&ovf, h->d_overflow.p, sizeof(int), hipMemcpyDeviceToHost));
+        *overflow = ovf;
+    });
+}
+
+int64_t record_bytes(int kp_cap) {
+    const int64_t raw = 8 + 2 * (int64_t)kp_cap * (int64_t)sizeof(orbfe_keypoint) + 2 * (int64_t)kp_cap * 32 +
+                        (int64_t)kp_cap * 9;
+    return (raw + 15) / 16 * 16;
+}
+
+int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes) {
+    return guarded([&] {
+        if (!h || !bytes) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
+        *bytes = record_bytes(h->geo.kp_cap);
+    });
+}
+
+int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0, int32_t n_pairs,
+                            void* hip_stream) {
+    return guarded([&] {
+        if (!h || !d_records) throw Error(ORBFE_EINVAL, "null argument");
+        if (pair0 < 0 || n_pairs < 0 || pair0 + n_pairs > h->last_pairs)
+            throw Error(ORBFE_EINVAL, "pair range outside the last stereo batch");
+        if (rec_bytes != record_bytes(h->geo.kp_cap)) throw Error(ORBFE_EINVAL, "record size does not match kp_cap");
+        if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
+        PackArgs a{h->d_count.p, h->d_kps.p, h->d_desc.p, h->d_uR.p, h->d_depth.p, h->d_status.p, h->geo.kp_cap,
+                   rec_bytes};
+        HIPCK(launch_pack(a, d_records, pair0, n_pairs, (hipStream_t)hip_stream));
+    });
+}
+
 int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
     return guarded([&] {
         if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");

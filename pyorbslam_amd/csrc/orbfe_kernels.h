@@ -40,6 +40,19 @@ struct StereoArgs {
     double bf;
 };
 
+// k_pack: per-pair fixed-capacity result records (see orbfe_batch_pack_device)
+struct PackArgs {
+    const int* count;
+    const orbfe_keypoint* kps;
+    const uint8_t* desc;
+    const float* u_right;
+    const float* depth;
+    const int8_t* status;
+    int kp_cap;
+    int64_t rec_bytes;
+};
+
+hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s);
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s, int variant = 0);
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,

@@ -14,6 +14,8 @@
 // those, see oracle/orb_oracle.cpp) and glibc's sinf/cosf polynomials (fma in double).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "orbfe_common.h"
 #include <type_traits>
 
@@ -2066,6 +2068,43 @@ hipError_t launch_shear(const Geo& g, const uint8_t* in, int64_t in_pitch, const
     if (n_images <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_shear, dim3((unsigned)((g.shear_bytes + 1023) / 1024), n_images), dim3(256), 0, s, g, in, in_pitch,
                        ws, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------- k_pack
+// One fixed-capacity record per stereo pair for the rank-0 gather of the batched-frames mode
+// (pyorbslam_amd/dist.py record layout): counts L, R (2 x i32) | keypoints L, R (cap x 24 B each) |
+// descriptors L, R (cap x 32 B each) | u_right, depth (cap x f32) | status (cap x i8).  Every region but
+// the last is a whole number of dwords at a dword offset: dword copies, the status bytes singly.
+__global__ __launch_bounds__(256) void k_pack(PackArgs a, uint8_t* __restrict__ out, int pair0) {
+    const int p = blockIdx.y, gp = pair0 + p;
+    uint8_t* rec = out + (int64_t)p * a.rec_bytes;
+    const int64_t cap = a.kp_cap;
+    const uint32_t* src[7] = {
+        (const uint32_t*)(a.count + 2 * (int64_t)gp),
+        (const uint32_t*)(a.kps + (2 * (int64_t)gp) * cap), (const uint32_t*)(a.kps + (2 * (int64_t)gp + 1) * cap),
+        (const uint32_t*)(a.desc + (2 * (int64_t)gp) * cap * 32), (const uint32_t*)(a.desc + (2 * (int64_t)gp + 1) * cap * 32),
+        (const uint32_t*)(a.u_right + gp * cap), (const uint32_t*)(a.depth + gp * cap)};
+    const int64_t words[7] = {2, cap * 6, cap * 6, cap * 8, cap * 8, cap, cap};
+    const int64_t nw = 2 + cap * 30;  // dwords of regions 0..6
+    for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw + cap; w += (int64_t)gridDim.x * 256) {
+        if (w >= nw) {  // status bytes
+            const int64_t i = w - nw;
+            rec[4 * nw + i] = (uint8_t)a.status[gp * cap + i];
+            continue;
+        }
+        int r = 0;
+        int64_t o = w;
+        while (o >= words[r]) o -= words[r++];
+        ((uint32_t*)rec)[w] = src[r][o];
+    }
+}
+
+hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s) {
+    if (n_pairs <= 0) return hipSuccess;
+    const int64_t items = 2 + (int64_t)a.kp_cap * 31;
+    const unsigned bx = (unsigned)std::min<int64_t>((items + 255) / 256, 64);
+    hipLaunchKernelGGL(k_pack, dim3(bx, n_pairs), dim3(256), 0, s, a, out, pair0);
     return hipGetLastError();
 }
 

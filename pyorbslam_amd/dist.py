@@ -2,10 +2,13 @@
 
 Pairs are independent (no cross-frame state in the front-end), so ranks exchange nothing on the data
 path.  The north star's only collective — collecting every pair's keypoints, descriptors and stereo
-results on rank 0 — is `gather_results`, a single gather of fixed-capacity byte records (RCCL over
-xGMI with backend "nccl", gloo on CPU).  It is not part of the timed step.
+results on rank 0 — is one gather of fixed-capacity byte records (RCCL over xGMI with backend "nccl",
+gloo on CPU): `pack_device` builds the records on the GPU with k_pack, `gather_records` gathers them,
+`timed_gather` times both for bench.py --gather (reported next to, not inside, the timed step).
 """
 from __future__ import annotations
+
+import time
 
 import numpy as np
 
@@ -69,10 +72,24 @@ def unpack(kp_cap: int, rec: np.ndarray) -> dict:
     return out
 
 
+def gather_records(records, dst: int = 0):
+    """records: (local_pairs, record_bytes) uint8 torch tensor of this rank — on the GPU with backend "nccl"
+    (RCCL over xGMI), on the CPU with gloo.  Every rank must pass the same shape (the batched-frames mode
+    gives every rank the same pair count; pad otherwise).  One collective, a gather to `dst`: returns the
+    (world * local_pairs, record_bytes) tensor on dst, rank-major = global pair order, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world == 1:
+        return records
+    outs = [torch.empty_like(records) for _ in range(world)] if rank == dst else None
+    dist.gather(records, gather_list=outs, dst=dst)
+    return torch.cat(outs, 0) if rank == dst else None
+
+
 def gather_results(records: np.ndarray, n_pairs_total: int, device=None, dst: int = 0):
-    """records: (local_pairs, record_bytes) uint8 of this rank.  Returns, on rank dst, the records of all
-    pairs in global pair order (None elsewhere).  One collective: an all_gather of equal-size buffers
-    (every rank pads to the largest shard), which both RCCL and gloo implement."""
+    """Host-array convenience over gather_records for uneven shards (shard()): every rank pads its
+    records to the largest shard.  Returns the records of all pairs in global pair order on dst."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -83,12 +100,64 @@ def gather_results(records: np.ndarray, n_pairs_total: int, device=None, dst: in
     t = torch.from_numpy(buf)
     if device is not None:
         t = t.to(device)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t)
+    full = gather_records(t, dst)
     if rank != dst:
         return None
-    full = []
-    for r in range(world):
-        _, n = shard(n_pairs_total, world, r)
-        full.append(outs[r].cpu().numpy()[:n])
-    return np.concatenate(full, axis=0)
+    full = full.cpu().numpy().reshape(world, maxn, rb)
+    return np.concatenate([full[r, :shard(n_pairs_total, world, r)[1]] for r in range(world)], axis=0)
+
+
+def pack_device(frontends, pairs_per_handle: int, out) -> None:
+    """Pack every pair of the handles' last stereo batches into `out` ((handles * pairs, record_bytes) uint8
+    device tensor) with k_pack, on the current stream (orbfe_batch_pack_device)."""
+    import ctypes as C
+    import torch
+    from ._lib import call
+    rb = out.shape[1]
+    st = torch.cuda.current_stream(out.device).cuda_stream
+    for i, f in enumerate(frontends):
+        call("orbfe_batch_pack_device", f.handle, C.c_void_p(out[i * pairs_per_handle].data_ptr()), rb, 0,
+             pairs_per_handle, C.c_void_p(st))
+
+
+def timed_gather(frontends, pairs_per_handle: int, device, world: int, rank: int, reps: int = 3) -> dict:
+    """Pack (k_pack) + gather to rank 0 of every pair's results, timed like the bench step (barrier +
+    synchronise on both sides, max over ranks); the records of rank 0's own first pair are checked
+    against orbfe_batch_fetch."""
+    import torch
+    import torch.distributed as dist
+    n_local = len(frontends) * pairs_per_handle
+    rb = record_bytes(frontends[0].kp_cap)
+    buf = torch.empty((n_local, rb), dtype=torch.uint8, device=device)
+    times = []
+    full = None
+    for _ in range(reps + 1):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        pack_device(frontends, pairs_per_handle, buf)
+        # RCCL gathers the device buffer in place; a gloo rehearsal (several ranks on one GPU) stages it
+        full = gather_records(buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu(), 0)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        times.append(time.perf_counter() - t0)
+    dt = float(np.mean(times[1:]))
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ok = None
+    if rank == 0:
+        u = unpack(frontends[0].kp_cap, full[0].cpu().numpy())
+        k, d = frontends[0].fetch_image(0)
+        s = frontends[0].fetch_stereo(0)
+        ok = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
+              and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["status"], s["status"]))
+        if not ok:
+            raise RuntimeError("gathered record of pair 0 differs from orbfe_batch_fetch")
+    return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "pairs_gathered": world * n_local,
+            "bytes_to_rank0": world * n_local * rb, "record_check": ok,
+            "what": "k_pack on every rank + one gather of the records to rank 0 (RCCL with nccl, gloo on CPU), "
+                    f"mean of {reps} after 1 warm-up, barrier + synchronize around each, max over ranks"}

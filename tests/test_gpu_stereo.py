@@ -224,3 +224,31 @@ def test_pair_path_empty_image():
     kl, dl, kr, dr = a.operator_kd_stereo(e, e, b, BF, np.float32(FX))
     assert len(kl) == 0 and dl.shape == (0, 0) and len(kr) == 0 and dr.shape == (0, 0)
     assert len(a.stereo_result["status"]) == 0
+
+
+def test_device_pack_records_match_fetch():
+    """k_pack (orbfe_batch_pack_device) builds the gather records of dist.py on the device: every field of
+    every pair decodes to what orbfe_batch_fetch / _fetch_stereo return."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd import dist as D
+    from pyorbslam_amd.batch import StereoFrontEnd
+    imgs = torch.from_numpy(synth.make_batch(3, seed0=70)).cuda()
+    fes = [StereoFrontEnd(max_pairs=3, lanes=1), StereoFrontEnd(max_pairs=3, lanes=2)]
+    for f in fes:
+        f.enqueue(imgs, 3)
+    torch.cuda.synchronize()
+    rb = D.record_bytes(fes[0].kp_cap)
+    buf = torch.zeros((6, rb), dtype=torch.uint8, device="cuda")
+    D.pack_device(fes, 3, buf)
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    for i, f in enumerate(fes):
+        for p in range(3):
+            u = D.unpack(f.kp_cap, host[3 * i + p])
+            kl, dl = f.fetch_image(2 * p)
+            kr, dr = f.fetch_image(2 * p + 1)
+            s = f.fetch_stereo(p)
+            assert u["kps_left"].tobytes() == kl.tobytes() and u["kps_right"].tobytes() == kr.tobytes()
+            assert np.array_equal(u["desc_left"], dl) and np.array_equal(u["desc_right"], dr)
+            for k in ("u_right", "depth", "status"):
+                assert np.array_equal(u[k], s[k]), k

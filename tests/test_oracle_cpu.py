@@ -322,3 +322,21 @@ def test_sheared_view_definition():
     flat = pad.ravel()
     assert np.array_equal(s.ravel(), flat[19 * 78 + 19: 19 * 78 + 19 + 1200])
     assert np.array_equal(s[0], lvl[0])  # row 0 is unsheared
+
+
+@pytest.mark.parametrize("name", ["kitti_synth_s0", "identical_s3"])
+def test_stereo_loop_restatement_matches_reference_golden(name, kitti_png):
+    """oracle/stereo_loop.py (the per-candidate-loop restatement bench.py times as the reference's CPU
+    path) gives the reference's outputs, types included."""
+    from oracle.stereo_loop import compute_stereo_matches_loop
+    L, R, params, g = golden_case_images(name, kitti_png)
+    exL, exR = O.OracleExtractor(**params), O.OracleExtractor(**params)
+    kl, dl = exL.extract(L)
+    kr, dr = exR.extract(R)
+    t = exL.tables()
+    u, d = compute_stereo_matches_loop(kl, kr, dl, dr, exL.sheared_pyramid(), exR.sheared_pyramid(), t["scale"],
+                                       t["inv_scale"], BF, np.float32(FX))
+    su, vu = stereo_oracle.encode(u)
+    sd, vd = stereo_oracle.encode(d)
+    assert np.array_equal(su, g["status"]) and np.array_equal(sd, g["status"])
+    assert np.array_equal(vu, g["u_right"]) and np.array_equal(vd, g["depth"])

@@ -1,7 +1,9 @@
 #!/bin/bash
-# GPU evidence for one revision of the default bench: parity tests, the bench line, a rocprofv3 kernel
-# trace of the same command, and the FETCH_SIZE / WRITE_SIZE passes (one pass each, as
-# MI355X_MICROARCH.md prescribes) that profiles/traffic.json is built from.
+# GPU evidence for one revision: parity tests, the default bench line (throughput + parity check of its own
+# workload + standalone per-stage roofline pass + cpu_baseline), the C3 frame-mode line, a gloo 2-rank
+# rehearsal with the timed device-side gather, a rocprofv3 kernel trace of the default bench command, and
+# FETCH_SIZE / WRITE_SIZE passes (one counter pass each, as MI355X_MICROARCH.md prescribes) over the
+# standalone pass only (--roofline-only) that profiles/traffic.json is built from.
 # usage (on the GPU box): bash tools/evidence.sh TAG      -> gpurun_out/ev_TAG/
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -9,7 +11,6 @@ tag=${1:-run}
 out=gpurun_out/ev_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 5"
 step() {  # name, timeout, command...
   local name=$1 to=$2; shift 2
   echo "== $name $(date +%T)"
@@ -19,9 +20,12 @@ step() {  # name, timeout, command...
   tail -n 3 "$out/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
-step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step bench 300 python $BENCH --cpu-sample 64
-step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ktrace" -o run -- python $BENCH --cpu-sample 0
-step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o run -- python bench.py --steps 4 --warmup 1 --cpu-sample 0
-step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o run -- python bench.py --steps 4 --warmup 1 --cpu-sample 0
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step bench 400 python bench.py
+step bench_frame 300 python bench.py --mode frame --steps 64 --warmup 1
+step bench_gather2_gloo 300 env ORBFE_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --pairs 64 --steps 5 --warmup 2 --gather --no-parity --roofline-steps 0
+step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ktrace" -o run -- python bench.py --cpu-sample 0
+step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o run -- python bench.py --roofline-only --roofline-steps 2
+step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o run -- python bench.py --roofline-only --roofline-steps 2
 echo "evidence done"
