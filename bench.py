@@ -121,7 +121,7 @@ def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, pro
     if procs > 1:
         ctx = mp.get_context("fork")
         barrier, queue = ctx.Barrier(procs), ctx.Queue()
-        per = 2
+        per = 4
         ps = [ctx.Process(target=_cpu_worker, args=([20_000 + per * i + j for j in range(per)], width, height, nfeatures,
                                                      barrier, queue)) for i in range(procs)]
         for p in ps:
@@ -270,7 +270,7 @@ def main():
     ap.add_argument("--blur-fork", type=int, default=0,
                     help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles "
                          "already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
-    ap.add_argument("--cpu-sample", type=int, default=12,
+    ap.add_argument("--cpu-sample", type=int, default=40,
                     help="pairs timed on 1 thread for cpu_baseline (0 = skip); the all-cores figure adds 2 per process")
     ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = this "
                     "job's CPU share, at most 16)")
