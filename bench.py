@@ -37,8 +37,9 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 STAGES = ["resize", "detect", "octree", "blur", "describe", "stereo"]
-STAGE_KERNELS = {"resize": "k_resize (x7 levels)", "detect": "k_detect", "octree": "k_octree", "blur": "k_blur",
-                 "describe": "k_describe", "stereo": "k_stereo_bucket + k_stereo"}
+STAGE_KERNELS = {"resize": "k_resize (x7 levels)", "detect": "k_detect", "octree": "k_octree", "blur": "(fused in k_orb)",
+                 "describe": "k_orb (IC angle + per-keypoint 7x7 blur + steered BRIEF)",
+                 "stereo": "k_stereo_bucket + k_stereo"}
 CAMERAS = {(1241, 376): ("kitti", "KITTI 1241x376"), (752, 480): ("euroc", "EuRoC 752x480")}
 
 
@@ -62,10 +63,11 @@ def algorithmic_bytes_per_pair(W, H, N=2000, nlevels=8):
         "detect": 2 * px,
         # the selected keypoints (4 B packed) written and read back
         "octree": 2 * 2 * N * 4,
-        # every level read once and its blurred copy written once
-        "blur": 2 * 2 * px,
-        # keypoint records + descriptors written (24 + 32 B per keypoint)
-        "describe": 2 * N * 56,
+        # fused into k_orb: no blurred level is written or read (kept as a 0-ms stage for the JSON layout)
+        "blur": 0,
+        # k_orb: each level's pixels around the keypoints (at most the level, read once) + the keypoint
+        # records and descriptors written (24 + 32 B per keypoint)
+        "describe": 2 * (px + N * 56),
         # both keypoint sets read + uR/depth written
         "stereo": 2 * N * 56 + N * 8,
     }
@@ -111,7 +113,7 @@ def _cpu_worker(seeds, width, height, nfeatures, barrier, queue):
 
 
 def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, procs: int):
-    """1 thread on `sample_pairs` pairs, then `procs` independent processes with 2 pairs each (all the
+    """1 thread on `sample_pairs` pairs, then `procs` independent processes with 4 pairs each (all the
     host cores this job may use).  Runs BEFORE anything initialises the GPU (the pool forks)."""
     import multiprocessing as mp
     n1, t1, te1 = _cpu_worker([10_000 + i for i in range(sample_pairs)], width, height, nfeatures, None, None)
@@ -271,7 +273,7 @@ def main():
                     help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles "
                          "already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
     ap.add_argument("--cpu-sample", type=int, default=40,
-                    help="pairs timed on 1 thread for cpu_baseline (0 = skip); the all-cores figure adds 2 per process")
+                    help="pairs timed on 1 thread for cpu_baseline (0 = skip); the all-cores figure adds 4 per process")
     ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = this "
                     "job's CPU share, at most 16)")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity check of the bench workload")
@@ -425,7 +427,8 @@ def main():
             out.update(parity)
         if stage_ms:
             dom = max(stage_ms, key=stage_ms.get)
-            ach = {s: per_stage_b[s] * P / (stage_ms[s] * 1e-3) / 1e9 for s in STAGES if stage_ms[s] > 0}
+            ach = {s: per_stage_b[s] * P / (stage_ms[s] * 1e-3) / 1e9 for s in STAGES
+                   if stage_ms[s] > 0 and per_stage_b[s] > 0}
             out["stage_ms_standalone_step"] = {k: round(v, 4) for k, v in stage_ms.items()}
             out["roofline"] = {
                 "bound": "hbm", "kernel": STAGE_KERNELS[dom], "stage": dom, "achieved": round(ach[dom], 3),

@@ -61,6 +61,7 @@ struct orbfe_ctx {
     DevBuf<CellGeo> d_cells;
     DevBuf<ResizeX> d_xt;
     DevBuf<uint32_t> d_mw;  // k_describe: [4 row shifts][31 x 9 window dwords] (disc byte mask, m10 weights)
+    DevBuf<uint32_t> d_orb; // k_orb: horizontal items of the sample disc + centroid slots (orb_tables)
     DevBuf<ResizeY> d_yt;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
@@ -385,6 +386,53 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.H = H;
 }
 
+// k_orb's per-lane tables (see k_orb in orbfe_kernels.hip).  Horizontal items: the (row pair m, 4-column
+// group gx) of the 43 x 40 horizontally blurred window that some BRIEF sample's 7 vertical taps read; a
+// sample lies at (row, col) with row^2 + col^2 <= (18.385 + 0.708)^2 (the pattern's largest radius,
+// ORBextractor.cpp:150-408, plus rint's rounding), blurred row o = row + 18 reads H rows o .. o + 6 at column
+// col + 21.  Centroid slots: every dword of staged rows 6 .. 36 that holds a byte of the umax disc
+// (ORBextractor.cpp:77-104), with its byte mask, the m10 byte weights u + 18 and the m01 row weight.
+std::vector<uint32_t> orb_tables(const int* umax) {
+    std::vector<uint32_t> t(kOrbTabWords, 0u);
+    bool need[44][40] = {};
+    const double R = 18.384776310850235 + 0.7072;
+    for (int row = -18; row <= 18; ++row)
+        for (int col = -18; col <= 18; ++col)
+            if (row * row + col * col <= R * R)
+                for (int k = 0; k < 7; ++k) need[row + 18 + k][col + 21] = true;
+    int n = 0;
+    for (int m = 0; m < 22; ++m)
+        for (int gx = 0; gx < 10; ++gx) {
+            bool any = false;
+            for (int rr = 0; rr < 2; ++rr)
+                for (int c = 0; c < 4; ++c) any |= need[2 * m + rr][4 * gx + c];
+            if (!any) continue;
+            if (n >= 192) throw Error(ORBFE_EINVAL, "k_orb: more than 192 horizontal items");
+            t[n++] = (uint32_t)(2 * m * 12 + gx) | ((uint32_t)(m * 10 + gx) << 16);
+        }
+    for (; n < 192; ++n) t[n] = ~0u;
+    uint32_t* cw = t.data() + 192;
+    int sl = 0;
+    for (int r = 0; r < 31; ++r) {
+        const int v = r - kHalfPatch, um = umax[v < 0 ? -v : v];
+        for (int d = (17 - um) / 4; d <= (um + 17) / 4; ++d) {
+            if (sl >= 256) throw Error(ORBFE_EINVAL, "k_orb: more than 256 centroid slots");
+            uint32_t mask = 0, wt = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * d + b - 17;
+                if (u >= -um && u <= um) mask |= 0xFFu << (8 * b);
+                wt |= (uint32_t)(u + 18) << (8 * b);
+            }
+            cw[4 * sl] = mask;
+            cw[4 * sl + 1] = wt;
+            cw[4 * sl + 2] = (uint32_t)((6 + r) * 12 + 2 + d);
+            cw[4 * sl + 3] = (uint32_t)r * 0x01010101u;
+            ++sl;
+        }
+    }
+    return t;
+}
+
 void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     if (W <= 0 || H <= 0 || max_images <= 0) throw Error(ORBFE_EINVAL, "bad reserve geometry");
     if (W != c.W || H != c.H) {
@@ -408,6 +456,11 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
             c.d_mw.ensure(mw.size());
             HIPCK(hipMemcpy(c.d_mw.p, mw.data(), mw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
+        {
+            const std::vector<uint32_t> ot = orb_tables(c.umax);
+            c.d_orb.ensure(ot.size());
+            HIPCK(hipMemcpy(c.d_orb.p, ot.data(), ot.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
         c.d_xt.ensure(c.xt.size());
         if (!c.xt.empty())
             HIPCK(hipMemcpy(c.d_xt.p, c.xt.data(), c.xt.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
@@ -420,7 +473,6 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         const Geo& g = c.geo;
         const size_t n = (size_t)max_images;
         c.d_ws.ensure(n * g.ws_bytes);
-        c.d_blur.ensure(n * g.blur_bytes);
         c.d_cell_count.ensure(n * std::max(g.ncells, 1));
         c.d_slots.ensure(n * g.slot_total);
         c.d_kd.ensure(n * g.key_total);
@@ -461,7 +513,6 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     const Geo& g = c.geo;
     const uint8_t* in = d_in + (int64_t)i0 * pitch;
     uint8_t* ws = c.d_ws.p + (int64_t)i0 * g.ws_bytes;
-    uint8_t* blur = c.d_blur.p + (int64_t)i0 * g.blur_bytes;
     int* cell_count = c.d_cell_count.p + (int64_t)i0 * g.ncells;
     uint32_t* slots = c.d_slots.p + (int64_t)i0 * g.slot_total;
     uint32_t* kd = c.d_kd.p + (int64_t)i0 * g.key_total;
@@ -474,36 +525,18 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     if (prof) prof_mark(c, s, 0);
     for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
     if (prof) prof_mark(c, s, 1);
-    if (fork_blur) {
-        // the blur of every level only needs the pyramid; it overlaps FAST and the octree, which are
-        // bound by VALU/LDS issue and latency rather than memory
-        const int k = lane + 1;  // side stream 0 serves the single-stream path, 1.. the lanes
-        if (!c.side_stream[k]) {
-            HIPCK(hipStreamCreateWithFlags(&c.side_stream[k], hipStreamNonBlocking));
-            HIPCK(hipEventCreateWithFlags(&c.ev_fork[k], hipEventDisableTiming));
-            HIPCK(hipEventCreateWithFlags(&c.ev_join[k], hipEventDisableTiming));
-        }
-        HIPCK(hipEventRecord(c.ev_fork[k], s));
-        HIPCK(hipStreamWaitEvent(c.side_stream[k], c.ev_fork[k], 0));
-        if (prof) prof_mark(c, c.side_stream[k], 7);
-        HIPCK(launch_blur(g, in, pitch, ws, blur, n, c.side_stream[k]));
-        if (prof) prof_mark(c, c.side_stream[k], 8);
-        HIPCK(hipEventRecord(c.ev_join[k], c.side_stream[k]));
-    }
+    (void)fork_blur;
+    (void)lane;
     if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
     if (prof) prof_mark(c, s, 2);
     HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
                         s));
     if (prof) prof_mark(c, s, 3);
-    if (fork_blur) {
-        HIPCK(hipStreamWaitEvent(s, c.ev_join[lane + 1], 0));  // join
-    } else {
-        if (prof) prof_mark(c, s, 7);
-        HIPCK(launch_blur(g, in, pitch, ws, blur, n, s));
-        if (prof) prof_mark(c, s, 8);
-    }
+    // the blur is fused into k_orb (each keypoint blurs its own neighbourhood): the blur stage is empty
+    if (prof) prof_mark(c, s, 7);
+    if (prof) prof_mark(c, s, 8);
     if (prof) prof_mark(c, s, 4);
-    HIPCK(launch_describe(g, in, pitch, ws, blur, lvl_kp, lvl_count, kps, desc, count, c.d_mw.p, n, s));
+    HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
     if (prof) prof_mark(c, s, 5);
 }
 
@@ -1184,11 +1217,18 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
-                    // variant 0 blur + describe, 1 blur, 2 describe, 4 describe with 4-wave workgroups,
-                    // 5 blur without its stores (probe)
-                    if (variant <= 1 || variant == 5)
+                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups; the unfused
+                    // pair for comparison: 1 k_blur, 2 k_describe (after a variant-1 run), 3 both, 4 k_describe
+                    // with 4-wave workgroups, 5 k_blur without its stores (probe)
+                    if (variant == 0 || variant == 8) {
+                        HIPCK(launch_orb(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
+                                         h->d_kps.p, h->d_desc.p, h->d_count.p, n, h->d_orb.p, s, variant));
+                        break;
+                    }
+                    h->d_blur.ensure((size_t)n * g.blur_bytes);
+                    if (variant == 1 || variant == 3 || variant == 5)
                         HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s, variant == 5));
-                    if (variant != 1 && variant != 5)
+                    if (variant == 2 || variant == 3 || variant == 4)
                         HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
                                               h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_mw.p,
                                               n, s, variant == 4 ? 4 : 0));

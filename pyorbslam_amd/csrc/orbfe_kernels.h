@@ -67,6 +67,12 @@ hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const 
 hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
                            const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
                            int* out_count, const uint32_t* mw, int n_images, hipStream_t s, int variant = 0);
+// fused IC angle + 7x7 blur of each keypoint's neighbourhood + steered BRIEF (replaces k_blur + k_describe)
+hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
+                      const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
+                      const uint32_t* tab, hipStream_t s, int variant = 0);
+// k_orb's item table (orb_tables on the host): 192 horizontal items + 256 centroid slots x 4 dwords
+constexpr int kOrbTabWords = 192 + 256 * 4;
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s);
 // sheared views of every level (GetImagePyramid), out: n_images x g.shear_bytes
 hipError_t launch_shear(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* out, int n_images,

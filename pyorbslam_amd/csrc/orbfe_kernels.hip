@@ -1596,6 +1596,280 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
     }
 }
 
+// ------------------------------------------------------------------------------- k_orb
+// IC_Angle + GaussianBlur 7x7 + steered BRIEF fused (ORBextractor.cpp:77-147, 1084-1089) for every kept
+// keypoint: the blurred level is never materialised.  A BRIEF sample lies within 18.385 px of the keypoint
+// (the pattern's largest radius) plus 0.71 px of rounding, so each keypoint needs the blur only on that
+// disc, i.e. the 7x7 taps of 43 x 43 unblurred pixels around it; the arithmetic is OpenCV's 8U fixed point
+// (SURVEY.md Appendix A.3): out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
+// One wavefront per keypoint, kOrbKpw consecutive keypoints of one level per wave (the next keypoint's
+// window loads are in flight while the current one is computed):
+//  * staging: rows cy-21 .. cy+21, columns cx-25 .. cx+22 as 12 dwords per row in LDS (byte j = column
+//    cx - 25 + j, the same layout for every keypoint), re-aligned with v_alignbyte from one buffer
+//    dwordx4 + one dword load per third of a row; keypoints whose window reaches past the level (reflect-101
+//    at the w x h clone's border, as the reference blurs a clone of the level) load byte by byte;
+//  * centroid on the staged unblurred bytes: the 213 dwords of the umax disc (rows 6 .. 36) from a table
+//    of (byte mask, m10 byte weights, dword, row weight), 3 v_dot4 each;
+//  * horizontal taps: the 189 (row pair, 4-column group) items the disc needs (a per-lane table), 10 v_dot4
+//    with shifted byte weights per row, stored row-pair interleaved as u16 pairs (dword = (H[2m][c], H[2m+1][c]));
+//  * BRIEF: lane j evaluates bits j + 64 i (i = 0..3); each of its 8 samples takes its vertical taps from
+//    4 interleaved dwords (2 ds_read2) with 4 v_dot2 whose weights depend on the sample row's parity; one
+//    ballot per 64 bits.
+constexpr int kOrbKpw = 4;             // keypoints per wavefront
+constexpr int kSrcRows = 43, kSrcDw = 12;
+constexpr int kHPairs = 22, kHGrp = 10, kHDw = 4 * kHGrp;  // H: 22 row pairs x 40 columns (dwords)
+constexpr int kStageItems = kSrcRows * 3;
+constexpr int kOrbHItems = 3;          // horizontal items per lane (189 of 192 used)
+constexpr int kOrbCSlots = 4;          // centroid slots per lane (213 of 256 used)
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// tab: [0, 192) horizontal items (src dword | hbuf uint4 index << 16, ~0 = none), then 256 centroid slots
+// as uint4 (byte mask, m10 byte weights, src dword, row weight byte-broadcast) — built by the host
+// (orbfe_host.hip: orb_tables).
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                                    const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
+                                                    const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
+                                                    uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
+                                                    const uint32_t* __restrict__ tab) {
+    __shared__ float4 s_pat[256];
+    __shared__ uint4 s_cw[64 * kOrbCSlots];
+    __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
+    __shared__ uint32_t s_h[WAVES][kHPairs * kHDw];       // horizontal taps, row-pair interleaved u16
+    const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
+    const int per = nb >> 3;
+    const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;  // XCD-aware: runs of waves per L2
+    const int img = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
+    const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(blk * WAVES + wid);
+    const float4 pat_r = threadIdx.x < 256 ? ((const float4*)c_pattern)[threadIdx.x] : float4{};
+    uint4 cw_r[(64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES)];
+#pragma unroll
+    for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
+        const int i = threadIdx.x + 64 * WAVES * k;
+        cw_r[k] = i < 64 * kOrbCSlots ? ((const uint4*)(tab + 192))[i] : uint4{};
+    }
+    uint32_t hit[kOrbHItems];
+#pragma unroll
+    for (int k = 0; k < kOrbHItems; ++k) hit[k] = tab[lane + 64 * k];
+    // wave -> (level, first keypoint) from the level capacities (host constants)
+    int l = 0, w0 = 0;
+    {
+        bool go = true;
+#pragma unroll
+        for (int i = 0; i + 1 < kMaxLevels; ++i) {
+            const int wc = (g.lv[i].kp_cap + kOrbKpw - 1) / kOrbKpw;
+            if (go && i + 1 < g.nlevels && wv >= w0 + wc) {
+                w0 += wc;
+                l = i + 1;
+            } else {
+                go = false;
+            }
+        }
+    }
+    const LevelGeo& L = g.lv[l];
+    const int* cnt = lvl_count + img * g.nlevels;
+    int pre[kMaxLevels + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxLevels; ++i) pre[i + 1] = pre[i] + (i < g.nlevels ? cnt[i] : 0);
+    if (blk == 0 && threadIdx.x == 0) out_count[img] = pre[kMaxLevels];
+    const int n_l = pre[l + 1] - pre[l];
+    const int k0 = kOrbKpw * (wv - w0);
+    const int nk = __builtin_amdgcn_readfirstlane(max(0, min(kOrbKpw, n_l - k0)));
+    const uint32_t mykey = lane < nk ? lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + k0 + lane] : 0u;
+    int stride;
+    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
+    uint32_t bias;
+    const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
+    uint32_t* src = s_src[wid];
+    uint32_t* hb = s_h[wid];
+    if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
+#pragma unroll
+    for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
+        const int i = threadIdx.x + 64 * WAVES * k;
+        if (i < 64 * kOrbCSlots) s_cw[i] = cw_r[k];
+    }
+    // the lane's staging items (row, third) as byte offsets from the window's first byte
+    uint32_t soff[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int it = min(lane + 64 * k, kStageItems - 1), r = it / 3, t = it - 3 * r;
+        soff[k] = (uint32_t)(r * stride + 16 * t);
+    }
+    __syncthreads();  // tables
+    uint4 rw[3];
+    uint32_t rx[3], rsh = 0;
+    auto key_of = [&](int j) { return (uint32_t)__builtin_amdgcn_readlane((int)mykey, j); };
+    // columns cx - 25 .. cx + 22 inside the level: dword staging (rows past the top / bottom are reflected
+    // per item); otherwise byte loads with reflect-101 in both directions
+    auto inside = [&](int cx) { return cx >= 25 && cx + 22 < L.w; };
+    auto row_off = [&](int k, int cy) {  // byte offset of item k's row and third from column 0 of row 0
+        const int it = min(lane + 64 * k, kStageItems - 1), r = it / 3, t = it - 3 * r;
+        return (uint32_t)(reflect101c(cy - 21 + r, L.h) * stride + 16 * t);
+    };
+    auto issue = [&](int cx, int cy) {
+        const bool rows_in = cy >= 21 && cy + 21 < L.h;
+        const uint32_t base = (uint32_t)(cx - 25) + bias + (rows_in ? (uint32_t)((cy - 21) * stride) : 0u);
+        rsh = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t a = base + (rows_in ? soff[k] : row_off(k, cy)), al = a & ~3u;
+            rsh |= (a & 3u) << (2 * k);
+            rw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, al, 0, 0));
+            rx[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 16u, 0, 0);
+        }
+    };
+    auto commit = [&]() {  // re-align each item by its own start's misalignment (rsh, 2 bits per item)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int it = lane + 64 * k;
+            if (it < kStageItems) {
+                const uint32_t sh = (rsh >> (2 * k)) & 3u;
+                const uint32_t w[5] = {rw[k].x, rw[k].y, rw[k].z, rw[k].w, rx[k]};
+                *(uint4*)(src + 4 * it) =  // item it = row it / 3, third it % 3: dwords 4 it .. 4 it + 3
+                    uint4{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                          __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
+            }
+        }
+    };
+    auto stage_border = [&](int cx, int cy) {  // reflect-101 at the level border, byte by byte
+        uint8_t* sb = (uint8_t*)src;
+        constexpr int NB = (kSrcRows * 4 * kSrcDw + 63) / 64, NR = 11;  // 33 bytes per lane, 11 loads in flight
+#pragma unroll 1
+        for (int j0 = 0; j0 < NB; j0 += NR) {
+            uint32_t v[NR];
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const int i = min(lane + 64 * (j0 + k), kSrcRows * 4 * kSrcDw - 1);
+                const int r = i / (4 * kSrcDw), c = i - r * (4 * kSrcDw);
+                const int y = reflect101c(cy - 21 + r, L.h), x = reflect101c(cx - 25 + c, L.w);
+                v[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(y * stride + x) + bias, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const int i = lane + 64 * (j0 + k);
+                if (i < kSrcRows * 4 * kSrcDw) sb[i] = (uint8_t)v[k];
+            }
+        }
+    };
+    int cx = 0, cy = 0;
+    if (nk > 0) {
+        const uint32_t k = key_of(0);
+        cx = (int)(k & 0xFFF);
+        cy = (int)((k >> 12) & 0xFFF);
+        if (inside(cx)) issue(cx, cy);
+    }
+    auto w4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | (b << 8) | (c << 16) | (d << 24); };
+    auto w2 = [](uint32_t a, uint32_t b) { return __builtin_bit_cast(us2, a | (b << 16)); };
+    for (int j = 0; j < nk; ++j) {
+        const uint32_t key = key_of(j);
+        const int score = (int)(key >> 24);
+        // ---- stage keypoint j: the previous keypoint's reads of src / hb are complete (waited before its
+        //      ballots, which precede this point)
+        wave_sync_lds();
+        if (inside(cx)) commit();
+        else stage_border(cx, cy);
+        wave_sync_lds();
+        const int ccx = cx, ccy = cy;
+        if (j + 1 < nk) {  // next keypoint's loads in flight during this one's compute
+            const uint32_t k = key_of(j + 1);
+            cx = (int)(k & 0xFFF);
+            cy = (int)((k >> 12) & 0xFFF);
+            if (inside(cx)) issue(cx, cy);
+        }
+        // ---- horizontal taps of the disc's (row pair, group) items
+#pragma unroll 1
+        for (int k = 0; k < kOrbHItems; ++k) {
+            if (hit[k] != ~0u) {
+                const uint32_t* q = src + (hit[k] & 0xFFFFu);
+                uint32_t h[2][4];
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    const uint32_t d0 = q[rr * kSrcDw], d1 = q[rr * kSrcDw + 1], d2 = q[rr * kSrcDw + 2];
+                    h[rr][0] = __builtin_amdgcn_udot4(d1, w4(56, 48, 34, 18),
+                                                      __builtin_amdgcn_udot4(d0, w4(0, 18, 34, 48), 0u, false), false);
+                    h[rr][1] = __builtin_amdgcn_udot4(
+                        d2, w4(18, 0, 0, 0),
+                        __builtin_amdgcn_udot4(d1, w4(48, 56, 48, 34), __builtin_amdgcn_udot4(d0, w4(0, 0, 18, 34), 0u, false),
+                                               false),
+                        false);
+                    h[rr][2] = __builtin_amdgcn_udot4(
+                        d2, w4(34, 18, 0, 0),
+                        __builtin_amdgcn_udot4(d1, w4(34, 48, 56, 48), __builtin_amdgcn_udot4(d0, w4(0, 0, 0, 18), 0u, false),
+                                               false),
+                        false);
+                    h[rr][3] = __builtin_amdgcn_udot4(d2, w4(48, 34, 18, 0),
+                                                      __builtin_amdgcn_udot4(d1, w4(18, 34, 48, 56), 0u, false), false);
+                }
+                *(uint4*)(hb + 4 * (hit[k] >> 16)) = uint4{h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
+                                                          h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
+            }
+        }
+        // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15)
+        uint32_t a10 = 0, a01 = 0, a1 = 0;
+#pragma unroll
+        for (int k = 0; k < kOrbCSlots; ++k) {
+            const uint4 cw = s_cw[lane + 64 * k];  // unused slots: mask 0
+            const uint32_t m = src[cw.z] & cw.x;
+            a10 = __builtin_amdgcn_udot4(m, cw.y, a10, false);
+            a01 = __builtin_amdgcn_udot4(m, cw.w, a01, false);
+            a1 = __builtin_amdgcn_udot4(m, 0x01010101u, a1, false);
+        }
+        const int m10 = wave_sum((int)a10 - 18 * (int)a1), m01 = wave_sum((int)a01 - 15 * (int)a1);
+        const float angle = fast_atan2((float)m01, (float)m10);
+        float b, a;
+        glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
+        wave_sync_lds();  // hb complete
+        // ---- steered BRIEF with the vertical taps per sample: sample (row, col) is blurred row o = row + 18
+        //      (H rows o .. o + 6), column c = col + 21; rint by the 1.5 * 2^23 trick (low mantissa bits
+        //      hold 0x400000 + rint(x))
+        const uint32_t cbase = 21u - __float_as_uint(12582912.0f);
+        uint64_t mine = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
+#pragma unroll 1
+        for (int i = 0; i < 4; ++i) {
+            const float4 pt = s_pat[lane + 64 * i];
+            uint32_t v2[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
+                const df2 mm = (df2){py, py} * (df2){a, -b};
+                const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
+                const uint32_t o = (__float_as_uint(rc.x) & 0xFFFFFFu) - 0x400000u + 18u;
+                const uint32_t c = __float_as_uint(rc.y) + cbase;
+                const uint32_t* p = hb + (o >> 1) * kHDw + c;
+                const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
+                const bool odd = o & 1u;
+                uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), odd ? w2(0, 18) : w2(18, 34), 32768u, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), odd ? w2(34, 48) : w2(48, 56), s, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), odd ? w2(56, 48) : w2(48, 34), s, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), odd ? w2(34, 18) : w2(18, 0), s, false);
+                v2[e] = s >> 16;
+            }
+            const uint64_t bb = __ballot(v2[0] < v2[1]);
+            mine = lane == i ? bb : mine;
+        }
+        const int o = pre[l] + k0 + j;
+        if (lane < 4) *(uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 8 * lane) = mine;
+        if (lane == 0) {
+            orbfe_keypoint kp;
+            kp.x = l ? __fmul_rn((float)ccx, L.scale) : (float)ccx;
+            kp.y = l ? __fmul_rn((float)ccy, L.scale) : (float)ccy;
+            kp.size = L.size;
+            kp.angle = angle;
+            kp.response = (float)score;
+            kp.octave = l;
+            out_kp[(int64_t)img * g.kp_cap + o] = kp;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------- k_shear
 // GetImagePyramid as the reference returns it (orb_extractor.cpp:30): the Mat -> ndarray caster ignores
 // Mat::step (opencv_type_casters.h:232-239), so row r of level l's (h, w) array is bytes
@@ -2054,6 +2328,27 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
         launch_describe_nw<4>(g, in, in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, mw, n_images, s);
     else
         launch_describe_nw<8>(g, in, in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, mw, n_images, s);
+    return hipGetLastError();
+}
+
+template <int NW>
+static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
+                          const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
+                          const uint32_t* tab, hipStream_t s) {
+    int waves = 0;  // most waves an image can need: kOrbKpw keypoints per wave, per level
+    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + kOrbKpw - 1) / kOrbKpw;
+    hipLaunchKernelGGL(k_orb<NW>, dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws, lvl_kp,
+                       lvl_count, out_kp, out_desc, out_count, tab);
+}
+
+// variant: waves per workgroup (0 = production)
+hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
+                      const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
+                      const uint32_t* tab, hipStream_t s, int variant) {
+    if (variant == 8)
+        launch_orb_nw<8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    else
+        launch_orb_nw<4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
     return hipGetLastError();
 }
 
