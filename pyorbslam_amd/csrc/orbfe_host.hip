@@ -1217,12 +1217,14 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
-                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups; the unfused
+                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups, 12 / 9: 2 / 8 keypoints
+                    // per wave; the unfused
                     // pair for comparison: 1 k_blur, 2 k_describe (after a variant-1 run), 3 both, 4 k_describe
                     // with 4-wave workgroups, 5 k_blur without its stores (probe)
-                    if (variant == 0 || variant == 8) {
+                    if (variant == 0 || variant == 8 || variant == 9 || variant == 10 || variant == 12) {
                         HIPCK(launch_orb(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
-                                         h->d_kps.p, h->d_desc.p, h->d_count.p, n, h->d_orb.p, s, variant));
+                                         h->d_kps.p, h->d_desc.p, h->d_count.p, n, h->d_orb.p, s,
+                                         variant == 12 ? 2 : variant));
                         break;
                     }
                     h->d_blur.ensure((size_t)n * g.blur_bytes);

@@ -1615,7 +1615,6 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8
 //  * BRIEF: lane j evaluates bits j + 64 i (i = 0..3); each of its 8 samples takes its vertical taps from
 //    4 interleaved dwords (2 ds_read2) with 4 v_dot2 whose weights depend on the sample row's parity; one
 //    ballot per 64 bits.
-constexpr int kOrbKpw = 4;             // keypoints per wavefront
 constexpr int kSrcRows = 43, kSrcDw = 12;
 constexpr int kHPairs = 22, kHGrp = 10, kHDw = 4 * kHGrp;  // H: 22 row pairs x 40 columns (dwords)
 constexpr int kStageItems = kSrcRows * 3;
@@ -1631,14 +1630,13 @@ __device__ __forceinline__ void wave_sync_lds() {
 // tab: [0, 192) horizontal items (src dword | hbuf uint4 index << 16, ~0 = none), then 256 centroid slots
 // as uint4 (byte mask, m10 byte weights, src dword, row weight byte-broadcast) — built by the host
 // (orbfe_host.hip: orb_tables).
-template <int WAVES>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+template <int WAVES, int kOrbKpw>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                     const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
                                                     const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                     const uint32_t* __restrict__ tab) {
-    __shared__ float4 s_pat[256];
-    __shared__ uint4 s_cw[64 * kOrbCSlots];
+    __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: (byte mask, m10 byte weights)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
     __shared__ uint32_t s_h[WAVES][kHPairs * kHDw];       // horizontal taps, row-pair interleaved u16
     const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1648,12 +1646,27 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wv = __builtin_amdgcn_readfirstlane(blk * WAVES + wid);
-    const float4 pat_r = threadIdx.x < 256 ? ((const float4*)c_pattern)[threadIdx.x] : float4{};
-    uint4 cw_r[(64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES)];
+    // the lane's 4 pattern point pairs (bits lane + 64 i) as int8 x0, y0, x1, y1 in one dword each, and its
+    // centroid slots' window dword + row weight (two 16-bit halves per register); the same for every keypoint
+    uint32_t pat[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 q = ((const float4*)c_pattern)[lane + 64 * i];
+        pat[i] = ((uint32_t)(int)q.x & 0xFFu) | (((uint32_t)(int)q.y & 0xFFu) << 8) | (((uint32_t)(int)q.z & 0xFFu) << 16) |
+                 ((uint32_t)(int)q.w << 24);
+    }
+    uint32_t cslot[kOrbCSlots / 2];
+#pragma unroll
+    for (int k = 0; k < kOrbCSlots / 2; ++k) {
+        const uint4 a = ((const uint4*)(tab + 192))[lane + 64 * (2 * k)], b = ((const uint4*)(tab + 192))[lane + 64 * (2 * k + 1)];
+        cslot[k] = (a.z | ((a.w & 0xFFu) << 9)) | ((b.z | ((b.w & 0xFFu) << 9)) << 16);
+    }
+    uint2 cw_r[(64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES)];
 #pragma unroll
     for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
         const int i = threadIdx.x + 64 * WAVES * k;
-        cw_r[k] = i < 64 * kOrbCSlots ? ((const uint4*)(tab + 192))[i] : uint4{};
+        const uint4 c = i < 64 * kOrbCSlots ? ((const uint4*)(tab + 192))[i] : uint4{};
+        cw_r[k] = uint2{c.x, c.y};
     }
     uint32_t hit[kOrbHItems];
 #pragma unroll
@@ -1690,18 +1703,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
     uint32_t* src = s_src[wid];
     uint32_t* hb = s_h[wid];
-    if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
 #pragma unroll
     for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
         const int i = threadIdx.x + 64 * WAVES * k;
         if (i < 64 * kOrbCSlots) s_cw[i] = cw_r[k];
-    }
-    // the lane's staging items (row, third) as byte offsets from the window's first byte
-    uint32_t soff[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int it = min(lane + 64 * k, kStageItems - 1), r = it / 3, t = it - 3 * r;
-        soff[k] = (uint32_t)(r * stride + 16 * t);
     }
     __syncthreads();  // tables
     uint4 rw[3];
@@ -1710,17 +1715,19 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // columns cx - 25 .. cx + 22 inside the level: dword staging (rows past the top / bottom are reflected
     // per item); otherwise byte loads with reflect-101 in both directions
     auto inside = [&](int cx) { return cx >= 25 && cx + 22 < L.w; };
-    auto row_off = [&](int k, int cy) {  // byte offset of item k's row and third from column 0 of row 0
-        const int it = min(lane + 64 * k, kStageItems - 1), r = it / 3, t = it - 3 * r;
-        return (uint32_t)(reflect101c(cy - 21 + r, L.h) * stride + 16 * t);
+    // the lane's staging item k: row it / 3, third it % 3 of the window (it = lane + 64 k)
+    auto row_off = [&](int k, int cy, bool rows_in) {  // byte offset from column cx - 25 of level row 0
+        const int it = min(lane + 64 * k, kStageItems - 1), r = (it * 171) >> 9, t = it - 3 * r;  // it / 3 for it < 129
+        const int y = rows_in ? cy - 21 + r : reflect101c(cy - 21 + r, L.h);
+        return (uint32_t)(y * stride + 16 * t);
     };
     auto issue = [&](int cx, int cy) {
         const bool rows_in = cy >= 21 && cy + 21 < L.h;
-        const uint32_t base = (uint32_t)(cx - 25) + bias + (rows_in ? (uint32_t)((cy - 21) * stride) : 0u);
+        const uint32_t base = (uint32_t)(cx - 25) + bias;
         rsh = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const uint32_t a = base + (rows_in ? soff[k] : row_off(k, cy)), al = a & ~3u;
+            const uint32_t a = base + row_off(k, cy, rows_in), al = a & ~3u;
             rsh |= (a & 3u) << (2 * k);
             rw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, al, 0, 0));
             rx[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 16u, 0, 0);
@@ -1816,10 +1823,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         uint32_t a10 = 0, a01 = 0, a1 = 0;
 #pragma unroll
         for (int k = 0; k < kOrbCSlots; ++k) {
-            const uint4 cw = s_cw[lane + 64 * k];  // unused slots: mask 0
-            const uint32_t m = src[cw.z] & cw.x;
+            const uint2 cw = s_cw[lane + 64 * k];  // unused slots: mask 0
+            const uint32_t sl = (cslot[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            const uint32_t m = src[sl & 0x1FFu] & cw.x;
             a10 = __builtin_amdgcn_udot4(m, cw.y, a10, false);
-            a01 = __builtin_amdgcn_udot4(m, cw.w, a01, false);
+            a01 = __builtin_amdgcn_udot4(m, (sl >> 9) * 0x01010101u, a01, false);  // row weight r = v + 15
             a1 = __builtin_amdgcn_udot4(m, 0x01010101u, a1, false);
         }
         const int m10 = wave_sum((int)a10 - 18 * (int)a1), m01 = wave_sum((int)a01 - 15 * (int)a1);
@@ -1834,11 +1842,12 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         uint64_t mine = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
 #pragma unroll 1
         for (int i = 0; i < 4; ++i) {
-            const float4 pt = s_pat[lane + 64 * i];
+            const uint32_t pq = i == 0 ? pat[0] : i == 1 ? pat[1] : i == 2 ? pat[2] : pat[3];
             uint32_t v2[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
+                const float px = (float)__builtin_amdgcn_sbfe((int)pq, 16 * e, 8);
+                const float py = (float)__builtin_amdgcn_sbfe((int)pq, 16 * e + 8, 8);
                 const df2 mm = (df2){py, py} * (df2){a, -b};
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
                 const uint32_t o = (__float_as_uint(rc.x) & 0xFFFFFFu) - 0x400000u + 18u;
@@ -2331,24 +2340,31 @@ hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, co
     return hipGetLastError();
 }
 
-template <int NW>
+template <int NW, int KPW>
 static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
                           const uint32_t* tab, hipStream_t s) {
-    int waves = 0;  // most waves an image can need: kOrbKpw keypoints per wave, per level
-    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + kOrbKpw - 1) / kOrbKpw;
-    hipLaunchKernelGGL(k_orb<NW>, dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws, lvl_kp,
-                       lvl_count, out_kp, out_desc, out_count, tab);
+    int waves = 0;  // most waves an image can need: KPW keypoints per wave, per level
+    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + KPW - 1) / KPW;
+    hipLaunchKernelGGL((k_orb<NW, KPW>), dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws,
+                       lvl_kp, lvl_count, out_kp, out_desc, out_count, tab);
 }
 
-// variant: waves per workgroup (0 = production)
+// variant (microbench): 0 = production (4 waves per workgroup, 4 keypoints per wave); 8: 8 waves; 2 / 9:
+// 2 / 8 keypoints per wave
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
                       const uint32_t* tab, hipStream_t s, int variant) {
     if (variant == 8)
-        launch_orb_nw<8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        launch_orb_nw<8, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    else if (variant == 2)
+        launch_orb_nw<4, 2>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    else if (variant == 10)
+        launch_orb_nw<4, 16>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    else if (variant == 9)
+        launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
     else
-        launch_orb_nw<4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
     return hipGetLastError();
 }
 
