@@ -1217,7 +1217,7 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
-                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups, 12 / 9: 2 / 8 keypoints
+                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups, 12 / 9 / 10: 2 / 4 / 16 keypoints
                     // per wave; the unfused
                     // pair for comparison: 1 k_blur, 2 k_describe (after a variant-1 run), 3 both, 4 k_describe
                     // with 4-wave workgroups, 5 k_blur without its stores (probe)

@@ -1631,11 +1631,12 @@ __device__ __forceinline__ void wave_sync_lds() {
 // as uint4 (byte mask, m10 byte weights, src dword, row weight byte-broadcast) — built by the host
 // (orbfe_host.hip: orb_tables).
 template <int WAVES, int kOrbKpw>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                     const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
                                                     const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                     const uint32_t* __restrict__ tab) {
+    __shared__ float4 s_pat[256];
     __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: (byte mask, m10 byte weights)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
     __shared__ uint32_t s_h[WAVES][kHPairs * kHDw];       // horizontal taps, row-pair interleaved u16
@@ -1646,15 +1647,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
     const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wv = __builtin_amdgcn_readfirstlane(blk * WAVES + wid);
-    // the lane's 4 pattern point pairs (bits lane + 64 i) as int8 x0, y0, x1, y1 in one dword each, and its
-    // centroid slots' window dword + row weight (two 16-bit halves per register); the same for every keypoint
-    uint32_t pat[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float4 q = ((const float4*)c_pattern)[lane + 64 * i];
-        pat[i] = ((uint32_t)(int)q.x & 0xFFu) | (((uint32_t)(int)q.y & 0xFFu) << 8) | (((uint32_t)(int)q.z & 0xFFu) << 16) |
-                 ((uint32_t)(int)q.w << 24);
-    }
+    // the lane's centroid slots: window dword + row weight (two 16-bit halves per register), the same for
+    // every keypoint
+    const float4 pat_r = threadIdx.x < 256 ? ((const float4*)c_pattern)[threadIdx.x] : float4{};
     uint32_t cslot[kOrbCSlots / 2];
 #pragma unroll
     for (int k = 0; k < kOrbCSlots / 2; ++k) {
@@ -1703,6 +1698,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
     const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
     uint32_t* src = s_src[wid];
     uint32_t* hb = s_h[wid];
+    if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
 #pragma unroll
     for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
         const int i = threadIdx.x + 64 * WAVES * k;
@@ -1842,12 +1838,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
         uint64_t mine = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
 #pragma unroll 1
         for (int i = 0; i < 4; ++i) {
-            const uint32_t pq = i == 0 ? pat[0] : i == 1 ? pat[1] : i == 2 ? pat[2] : pat[3];
+            const float4 pt = s_pat[lane + 64 * i];
             uint32_t v2[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const float px = (float)__builtin_amdgcn_sbfe((int)pq, 16 * e, 8);
-                const float py = (float)__builtin_amdgcn_sbfe((int)pq, 16 * e + 8, 8);
+                const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
                 const df2 mm = (df2){py, py} * (df2){a, -b};
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
                 const uint32_t o = (__float_as_uint(rc.x) & 0xFFFFFFu) - 0x400000u + 18u;
@@ -2350,8 +2345,8 @@ static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, con
                        lvl_kp, lvl_count, out_kp, out_desc, out_count, tab);
 }
 
-// variant (microbench): 0 = production (4 waves per workgroup, 4 keypoints per wave); 8: 8 waves; 2 / 9:
-// 2 / 8 keypoints per wave
+// variant (microbench): 0 = production (4 waves per workgroup, 8 keypoints per wave: 953 -> 914 us per 256
+// pairs against 4, same-box A/B); 8: 8 waves; 2 / 9 / 10: 2 / 4 / 16 keypoints per wave
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
                       const uint32_t* tab, hipStream_t s, int variant) {
@@ -2362,9 +2357,9 @@ hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const u
     else if (variant == 10)
         launch_orb_nw<4, 16>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
     else if (variant == 9)
-        launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
-    else
         launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    else
+        launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
     return hipGetLastError();
 }
 
