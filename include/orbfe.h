@@ -132,6 +132,15 @@ int orbfe_frame_fetch_stereo(orbfe_handle h, float* u_right, float* depth, int8_
  * the size. */
 int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* out, int32_t* w_out, int32_t* h_out);
 
+/* cv::undistortPoints(pts, K, D, noArray(), K) as Frame.undistort_keypoints (Frame.py:306) and
+ * Tracking.compute_image_bounds (Tracking.py:132) call it: OpenCV 4.x's 5-iteration fixed point in double
+ * (k_undistort).  K4 = (fx, fy, cx, cy) and dist = (k1, k2, p1, p2[, k3]) as float (the reference keeps
+ * mK and mDistCoef in float32); xy: n points at `stride` floats apart (x, y first); out: n x 2 floats.
+ * Parity is unpinned: OpenCV is absent and the reference's distorted branch is unreachable (NameError
+ * on `mvKeys` at Frame.py:299); DESIGN.md §2 states the semantics followed. */
+int orbfe_undistort_points(orbfe_handle h, const float* K4, const float* dist, int32_t n_dist, const float* xy, int32_t n,
+                           int32_t stride, float* out);
+
 /* ---- device batch API (bench / batched-frames mode) ----------------------------------------
  * Images are device-resident, n_images x (height x img_pitch) u8, stereo pair p = images
  * (2p, 2p+1) = (left, right).  Results stay on device in handle-owned buffers. */

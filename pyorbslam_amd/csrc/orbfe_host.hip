@@ -116,6 +116,7 @@ struct orbfe_ctx {
     // per-frame stereo path (orbfe_frame_extract): both images staged in d_in (pitch frame_pitch), the
     // sheared pyramids in d_shear, every result copied into the pinned h_frame before one synchronisation
     DevBuf<uint8_t> d_shear;
+    DevBuf<float> d_uin, d_uout;  // orbfe_undistort_points scratch
     HostBuf<uint8_t> h_frame;
     int64_t frame_pitch = 0;
     bool have_frame = false, frame_pyr = false;
@@ -892,6 +893,24 @@ int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* ou
             h->frame_pyr = true;
         }
         std::memcpy(out, h->h_frame.p + h->fo_shear + side * (size_t)g.shear_bytes + L.shear_off, (size_t)L.w * L.h);
+    });
+}
+
+int orbfe_undistort_points(orbfe_handle h, const float* K4, const float* dist, int32_t n_dist, const float* xy, int32_t n,
+                           int32_t stride, float* out) {
+    return guarded([&] {
+        if (!h || !K4 || !dist || (n > 0 && (!xy || !out))) throw Error(ORBFE_EINVAL, "null argument");
+        if (n < 0 || stride < 2) throw Error(ORBFE_EINVAL, "bad point count / stride");
+        if (n_dist != 4 && n_dist != 5) throw Error(ORBFE_EINVAL, "distortion must be (k1, k2, p1, p2[, k3])");
+        if (n == 0) return;
+        UndistortArgs a{K4[0], K4[1], K4[2], K4[3], dist[0], dist[1], dist[2], dist[3], n_dist == 5 ? dist[4] : 0.f};
+        hipStream_t s = own(*h);
+        h->d_uin.ensure((size_t)n * stride);
+        h->d_uout.ensure((size_t)n * 2);
+        HIPCK(hipMemcpyAsync(h->d_uin.p, xy, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, s));
+        HIPCK(launch_undistort(h->d_uin.p, n, stride, h->d_uout.p, a, s));
+        HIPCK(hipMemcpyAsync(out, h->d_uout.p, (size_t)n * 2 * sizeof(float), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
     });
 }
 

@@ -53,6 +53,13 @@ struct PackArgs {
 };
 
 hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s);
+// k_undistort: pinhole K (float in the reference: mK is float32) + distortion (k1, k2, p1, p2[, k3])
+struct UndistortArgs {
+    double fx, fy, cx, cy;
+    double k1, k2, p1, p2, k3;
+};
+hipError_t launch_undistort(const float* xy_in, int n, int stride_in, float* xy_out, const UndistortArgs& a,
+                            hipStream_t s);
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s, int variant = 0);
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,

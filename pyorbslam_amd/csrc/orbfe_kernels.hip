@@ -1874,6 +1874,46 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     }
 }
 
+// ------------------------------------------------------------------------------- k_undistort
+// cv::undistortPoints(pts, K, D, R = noArray(), P = K) (OpenCV 4.x cvUndistortPointsInternal), the call of
+// Frame.undistort_keypoints (Frame.py:306) and Tracking.compute_image_bounds (Tracking.py:132): in double,
+// x0 = (u - cx) / fx, y0 = (v - cy) / fy, then 5 fixed-point iterations (TermCriteria(COUNT, 5, 0.01))
+//   r2 = x^2 + y^2, icdist = 1 / (1 + ((k3 r2 + k2) r2 + k1) r2)   (k4..k6 = 0: 4- or 5-coefficient models)
+//   dx = 2 p1 x y + p2 (r2 + 2 x^2), dy = p1 (r2 + 2 y^2) + 2 p2 x y, x = (x0 - dx) icdist, y = (y0 - dy) icdist
+// (a negative icdist stops at the normalised input, as OpenCV >= 4.2 does), then P = K back to pixels, stored
+// as float.  One thread per point; no FMA contraction (built with -ffp-contract=off).
+__global__ __launch_bounds__(256) void k_undistort(const float* __restrict__ xy_in, int n, int stride_in,
+                                                   float* __restrict__ xy_out, UndistortArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double u = xy_in[(int64_t)i * stride_in], v = xy_in[(int64_t)i * stride_in + 1];
+    const double ifx = 1. / a.fx, ify = 1. / a.fy;
+    const double x0 = (u - a.cx) * ifx, y0 = (v - a.cy) * ify;
+    double x = x0, y = y0;
+    for (int it = 0; it < 5; ++it) {
+        const double r2 = x * x + y * y;
+        const double icdist = 1. / (1. + ((a.k3 * r2 + a.k2) * r2 + a.k1) * r2);
+        if (icdist < 0) {
+            x = x0;
+            y = y0;
+            break;
+        }
+        const double dx = 2 * a.p1 * x * y + a.p2 * (r2 + 2 * x * x);
+        const double dy = a.p1 * (r2 + 2 * y * y) + 2 * a.p2 * x * y;
+        x = (x0 - dx) * icdist;
+        y = (y0 - dy) * icdist;
+    }
+    xy_out[2 * (int64_t)i] = (float)(x * a.fx + a.cx);
+    xy_out[2 * (int64_t)i + 1] = (float)(y * a.fy + a.cy);
+}
+
+hipError_t launch_undistort(const float* xy_in, int n, int stride_in, float* xy_out, const UndistortArgs& a,
+                            hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, s, xy_in, n, stride_in, xy_out, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------- k_shear
 // GetImagePyramid as the reference returns it (orb_extractor.cpp:30): the Mat -> ndarray caster ignores
 // Mat::step (opencv_type_casters.h:232-239), so row r of level l's (h, w) array is bytes

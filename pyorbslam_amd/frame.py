@@ -173,11 +173,56 @@ def frame_copy(self, frame):
     return new
 
 
+_undistort_local = None
+
+
+def undistort_points(xy, mK, mDistCoef) -> np.ndarray:
+    """cv2.undistortPoints(xy, mK, mDistCoef, None, mK) on the GPU (k_undistort): (n, 2) float32 -> (n, 2)
+    float32.  Used by the Frame drop-in below and usable for Tracking.compute_image_bounds
+    (Tracking.py:131-133)."""
+    global _undistort_local
+    import threading
+    if _undistort_local is None:
+        _undistort_local = threading.local()
+    h = getattr(_undistort_local, "h", None)
+    if h is None:
+        from . import _lib
+        h = C.c_void_p()
+        call("orbfe_create", C.byref(_lib.make_params(2000, 1.2, 8, 20, 7)), C.byref(h))
+        _undistort_local.h = h
+    xy = np.ascontiguousarray(np.asarray(xy, np.float32).reshape(-1, 2))
+    K = np.asarray(mK, np.float32)
+    K4 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], np.float32)
+    d = np.ascontiguousarray(np.asarray(mDistCoef, np.float32).ravel())
+    out = np.empty_like(xy)
+    call("orbfe_undistort_points", h, ptr(K4), ptr(d), len(d), ptr(xy), len(xy), 2, ptr(out))
+    return out
+
+
+def undistort_keypoints(self):
+    """Frame.undistort_keypoints (Frame.py:293-322).  Zero k1: mvKeysUn is mvKeys (the reference's only
+    reachable branch).  Otherwise the reference raises NameError (it reads the undefined `mvKeys` at
+    Frame.py:299); the drop-in does what that code means — cv2.undistortPoints(pts, mK, mDistCoef, None,
+    mK) on the keypoints, on the GPU, new KeyPoints with the other fields kept — and assigns
+    self.mvKeysUn (which the reference computes and returns but never stores) as well as returning it."""
+    if self.mDistCoef[0][0] == 0:
+        self.mvKeysUn = self.mvKeys
+        return
+    KeyPoint = _keypoint_cls(self)
+    pts = np.array([kp.pt for kp in self.mvKeys], np.float32).reshape(-1, 2)
+    und = undistort_points(pts, self.mK, self.mDistCoef) if len(pts) else pts
+    self.mvKeysUn = [KeyPoint(x=float(und[i, 0]), y=float(und[i, 1]), size=kp.size, angle=kp.angle,
+                              response=kp.response, octave=kp.octave, class_id=getattr(kp, "class_id", -1))
+                     for i, kp in enumerate(self.mvKeys)]
+    return self.mvKeysUn
+
+
 def install(frame_cls, copy: bool = True, pair: bool = True) -> None:
-    """Replace Frame.compute_stereo_matches (Frame.py:161), unless pair=False Frame.ExtractORB
-    (Frame.py:114: both images in one enqueue) and unless copy=False Frame.copy (Frame.py:75) of the
-    reference class in place."""
+    """Replace Frame.compute_stereo_matches (Frame.py:161), Frame.undistort_keypoints (Frame.py:293), unless
+    pair=False Frame.ExtractORB (Frame.py:114: both images in one enqueue) and unless copy=False Frame.copy
+    (Frame.py:75) of the reference class in place."""
     frame_cls.compute_stereo_matches = compute_stereo_matches
+    frame_cls.undistort_keypoints = undistort_keypoints
     if pair:
         frame_cls.ExtractORB = extract_orb
     if copy:

@@ -252,3 +252,41 @@ def test_device_pack_records_match_fetch():
             assert np.array_equal(u["desc_left"], dl) and np.array_equal(u["desc_right"], dr)
             for k in ("u_right", "depth", "status"):
                 assert np.array_equal(u[k], s[k]), k
+
+
+def test_undistort_points_matches_opencv_restatement():
+    """k_undistort against oracle/undistort_oracle.py (cv::undistortPoints restated; parity with OpenCV
+    itself is unpinned: OpenCV is absent and the reference's distorted branch is unreachable)."""
+    from oracle.undistort_oracle import undistort_points as ref
+    rng = np.random.default_rng(5)
+    xy = np.stack([rng.uniform(0, 752, 3000), rng.uniform(0, 480, 3000)], 1).astype(np.float32)
+    xy[:4] = [[0, 0], [752, 0], [0, 480], [752, 480]]  # Tracking.compute_image_bounds' corners
+    K = np.eye(3, dtype=np.float32)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = 458.654, 457.296, 367.215, 248.375  # EuRoC cam0
+    for dist in ([-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05],        # EuRoC cam0 (4 coefficients)
+                 [-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05, 0.01],  # + k3
+                 [-2.0, -5.0, 0.0, 0.0],                                      # icdist < 0 at the corners
+                 [0.0, 0.0, 0.0, 0.0]):
+        got = F.undistort_points(xy, K, np.array(dist, np.float32).reshape(-1, 1))
+        want = ref(xy, K, dist)
+        assert got.dtype == np.float32 and np.array_equal(got, want), dist
+
+
+def test_undistort_keypoints_drop_in():
+    from oracle.undistort_oracle import undistort_points as ref
+    import seq_harness as H
+
+    class Fr(H.SeqFrame):
+        pass
+
+    F.install(Fr)
+    s = H.settings(synth.KITTI_CAM)
+    dist = np.array([[-0.28], [0.07], [0.0002], [0.00002]], np.float32)
+    L, R = synth.make_pair(9)
+    f = Fr(L, R, 0.0, ORBextractor(**KITTI), ORBextractor(**KITTI), None, s["mK"], dist, s["mbf"], s["mThDepth"],
+           H.frame_args(s, 1241, 376))
+    pts = np.array([k.pt for k in f.mvKeys], np.float32)
+    want = ref(pts, s["mK"], dist.ravel())
+    assert len(f.mvKeysUn) == f.N
+    assert all(u.pt == (float(w[0]), float(w[1])) and u.octave == k.octave and u.angle == k.angle
+               for u, k, w in zip(f.mvKeysUn, f.mvKeys, want))
