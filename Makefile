@@ -5,10 +5,12 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -Wall \
             -munsafe-fp-atomics -Wno-unused-result
 SRC := pyorbslam_amd/csrc/orbfe_kernels.hip pyorbslam_amd/csrc/orbfe_host.hip pyorbslam_amd/csrc/orbfe_vocab.hip
+CSRC := pyorbslam_amd/csrc/orbfe_png.cpp
 HDR := pyorbslam_amd/csrc/orbfe_common.h pyorbslam_amd/csrc/orbfe_kernels.h pyorbslam_amd/csrc/orbfe_host_util.h include/orbfe.h \
        pyorbslam_amd/csrc/brief_pattern.inc
 LIB := pyorbslam_amd/_lib/liborbfe.so
-OBJ := $(patsubst pyorbslam_amd/csrc/%.hip,pyorbslam_amd/_lib/%.o,$(SRC))
+OBJ := $(patsubst pyorbslam_amd/csrc/%.hip,pyorbslam_amd/_lib/%.o,$(SRC)) \
+       $(patsubst pyorbslam_amd/csrc/%.cpp,pyorbslam_amd/_lib/%.o,$(CSRC))
 
 all: $(LIB) oracle
 
@@ -16,8 +18,13 @@ pyorbslam_amd/_lib/%.o: pyorbslam_amd/csrc/%.hip $(HDR)
 	@mkdir -p pyorbslam_amd/_lib
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+# host-only C++ (ingest): no device code
+pyorbslam_amd/_lib/%.o: pyorbslam_amd/csrc/%.cpp $(HDR)
+	@mkdir -p pyorbslam_amd/_lib
+	$(HIPCC) -O3 -std=c++17 -fPIC -Wall -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c -o $@ $<
+
 $(LIB): $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) -lz -lpthread
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -242,6 +242,16 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t* out);
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);
 
+/* ---- image ingest (stereo_kitti.py:42-43: cv2.imread(path, cv2.IMREAD_GRAYSCALE)) ------------------
+ * PNG (8-bit grey / RGB / grey+alpha / RGBA, non-interlaced) to 8-bit grey, decoded natively (zlib inflate
+ * + row unfiltering; colour converted with libpng's rgb_to_gray fixed-point weights as OpenCV requests).
+ * orbfe_png_decode: one image from memory; out = NULL returns the size only; `stride` bytes per out row.
+ * orbfe_png_read_batch: n files of one size decoded by `threads` host threads into out (n x h x w,
+ * contiguous), e.g. pinned staging for one host-to-device copy of a batch of stereo pairs. */
+int orbfe_png_decode(const uint8_t* data, int64_t size, uint8_t* out, int64_t stride, int32_t* width, int32_t* height);
+int orbfe_png_read_batch(const char* const* paths, int32_t n, int32_t width, int32_t height, uint8_t* out,
+                         int32_t threads);
+
 /* ---- live stage timing --------------------------------------------------------------------------
  * While profiling is on, every batch enqueued on the handle records HIP events around its stages:
  * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 blur (k_blur, timed on the side

@@ -61,6 +61,8 @@ SIGNATURES = {
     "orbfe_frame_pyramid": [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
     "orbfe_undistort_points": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
                                C.c_void_p],
+    "orbfe_png_decode": [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
+    "orbfe_png_read_batch": [C.POINTER(C.c_char_p), C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32],
     "orbfe_batch_reserve": [C.c_void_p, C.c_int32, C.c_int32, C.c_int32],
     "orbfe_extract_batch_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p],
     "orbfe_stereo_batch_device": [C.c_void_p, C.c_int32, C.c_double, C.c_float, C.c_void_p],
