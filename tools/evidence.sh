@@ -22,6 +22,7 @@ step() {  # name, timeout, command...
 }
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 step bench 400 python bench.py
+step bench_euroc 300 python bench.py --width 752 --height 480 --nfeatures 1000 --cpu-sample 12
 step bench_frame 300 python bench.py --mode frame --steps 64 --warmup 1
 step bench_gather2_gloo 300 env ORBFE_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --pairs 64 --steps 5 --warmup 2 --gather --no-parity --roofline-steps 0
