@@ -11,7 +11,7 @@ import json
 import sys
 
 STAGES = {"resize": ["k_resize"], "detect": ["k_detect"], "octree": ["k_octree"],
-          "blur": ["k_blur"], "describe": ["k_describe"], "stereo": ["k_stereo_bucket", "k_stereo"]}
+          "blur": ["k_blur"], "describe": ["k_orb", "k_describe"], "stereo": ["k_stereo_bucket", "k_stereo"]}
 
 
 def per_kernel(d, counter):
