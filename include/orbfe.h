@@ -238,6 +238,18 @@ int orbfe_hamming_csr(orbfe_handle h, const uint8_t* query_desc, int32_t n_query
  * reference's ~10 us Python call; batches go through the kernels above / below). */
 int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t* out);
 
+/* Frame.get_features_in_area (Frame.py:373-416) for n_q queries at once, on the host: the frame's 64 x 48
+ * grid (Frame.assign_features_to_grid, Frame.py:152-159) as CSR (cell (ix, iy) = cell_off[ix * rows + iy]
+ * .. cell_off[ix * rows + iy + 1) into cell_idx, the reference's list order), the keypoints' pt (double
+ * values of the Python floats) and octave, frame4 = (mnMinX, mnMinY, mfGridElementWidthInv,
+ * mfGridElementHeightInv); query q = (x, y, r, min_level, max_level) in double.  Candidates of query q:
+ * out_idx[out_off[q] .. out_off[q + 1]), in the reference's order.  ORBFE_ECAPACITY if more than cap
+ * (out_off[n_q] then holds the total).  The ORBMatcher drop-in uses it when every operand is a double. */
+int orbfe_grid_query(const int32_t* cell_off, const int32_t* cell_idx, int32_t cols, int32_t rows, const double* kp_x,
+                     const double* kp_y, const int32_t* kp_oct, int32_t n_kp, const double* frame4, int32_t n_q,
+                     const double* qx, const double* qy, const double* qr, const int32_t* qmin, const int32_t* qmax,
+                     int32_t* out_off, int32_t* out_idx, int64_t cap);
+
 /* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);

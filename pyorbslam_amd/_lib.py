@@ -17,6 +17,7 @@ LIB_PATH = Path(os.environ.get("ORBFE_LIB") or Path(__file__).resolve().parent /
 ORBFE_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ESTATE", -6: "EOVERFLOW", -7: "EFORMAT",
           -8: "EREJECT"}
+ORBFE_ECAPACITY = -4
 ORBFE_EFORMAT = -7
 ORBFE_EREJECT = -8
 
@@ -79,6 +80,9 @@ SIGNATURES = {
     "orbfe_hamming_csr": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                           C.c_void_p],
     "orbfe_descriptor_distance": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],
+    "orbfe_grid_query": [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                         C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                         C.c_void_p, C.c_int64],
     "orbfe_hamming_matrix": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p],
     "orbfe_profile_begin": [C.c_void_p, C.c_int32],
     "orbfe_profile_read": [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)],

@@ -1098,6 +1098,52 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b, int32_t* out) 
     });
 }
 
+int orbfe_grid_query(const int32_t* cell_off, const int32_t* cell_idx, int32_t cols, int32_t rows, const double* kp_x,
+                     const double* kp_y, const int32_t* kp_oct, int32_t n_kp, const double* frame4, int32_t n_q,
+                     const double* qx, const double* qy, const double* qr, const int32_t* qmin, const int32_t* qmax,
+                     int32_t* out_off, int32_t* out_idx, int64_t cap) {
+    return guarded([&] {
+        if (!cell_off || !frame4 || (n_q > 0 && (!qx || !qy || !qr || !qmin || !qmax || !out_off)))
+            throw Error(ORBFE_EINVAL, "null argument");
+        if (cols <= 0 || rows <= 0 || n_q < 0 || n_kp < 0) throw Error(ORBFE_EINVAL, "bad sizes");
+        const double minX = frame4[0], minY = frame4[1], invW = frame4[2], invH = frame4[3];
+        int64_t n = 0;
+        out_off[0] = 0;
+        for (int q = 0; q < n_q; ++q) {
+            const double x = qx[q], y = qy[q], r = qr[q];
+            const int lo = qmin[q], hi = qmax[q];
+            // Frame.get_features_in_area (Frame.py:373-416) in the Python floats' double arithmetic; int()
+            // truncates toward zero like the C conversion
+            const int x0 = std::max(0, (int)((x - minX - r) * invW));
+            const int x1 = std::min(cols - 1, (int)((x - minX + r) * invW));
+            const int y0 = std::max(0, (int)((y - minY - r) * invH));
+            const int y1 = std::min(rows - 1, (int)((y - minY + r) * invH));
+            if (x0 < cols && x1 >= 0 && y0 < rows && y1 >= 0) {
+                const bool check = lo > 0 || hi >= 0;
+                for (int ix = x0; ix <= x1; ++ix)
+                    for (int iy = y0; iy <= y1; ++iy) {
+                        const int c = ix * rows + iy;
+                        for (int k = cell_off[c]; k < cell_off[c + 1]; ++k) {
+                            const int g = cell_idx[k];
+                            if (g < 0 || g >= n_kp) throw Error(ORBFE_EINVAL, "grid index out of range");
+                            if (check) {
+                                if (kp_oct[g] < lo) continue;
+                                if (hi >= 0 && kp_oct[g] > hi) continue;
+                            }
+                            if (std::fabs(kp_x[g] - x) < r && std::fabs(kp_y[g] - y) < r) {
+                                if (n < cap) out_idx[n] = g;
+                                ++n;
+                            }
+                        }
+                    }
+            }
+            if (n > INT32_MAX) throw Error(ORBFE_ECAPACITY, "too many candidates");
+            out_off[q + 1] = (int32_t)n;
+        }
+        if (n > cap) throw Error(ORBFE_ECAPACITY, "candidate buffer too small (out_off[n_q] holds the need)");
+    });
+}
+
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out) {
     return guarded([&] {

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
+import weakref
 
 import numpy as np
 
@@ -97,6 +98,81 @@ def hamming_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return out
 
 
+# ---------------------------------------------------------------------------------------- grid queries
+# Frame.get_features_in_area (Frame.py:373-416) for all the queries of a search at once (orbfe_grid_query,
+# host code in liborbfe).  Used when every operand is a double (Python float, np.float64, or a 1-element
+# float64 array — the types the reference's tracking loop produces); any other operand type (a float32
+# projection evaluates in float32 under NumPy 2's promotion rules) goes through the frame's own method.
+_grid_cache = weakref.WeakKeyDictionary()
+_F64 = (float, np.float64)
+
+
+def _is_f64(v) -> bool:
+    return type(v) in _F64 or (type(v) is np.ndarray and v.dtype == np.float64 and v.size == 1)
+
+
+def _frame_grid(frame):
+    """(cell_off, cell_idx, kp_x, kp_y, kp_oct, frame4) of a frame, cached while its grid / keypoints are
+    the same objects; None if the frame's grid parameters are not plain doubles."""
+    try:
+        ent = _grid_cache.get(frame)
+    except TypeError:
+        return None
+    key = (id(frame.mGrid), id(frame.mvKeysUn), frame.N)
+    if ent is not None and ent[0] == key:
+        return ent[1]
+    f4 = (frame.mnMinX, frame.mnMinY, frame.mfGridElementWidthInv, frame.mfGridElementHeightInv)
+    if not all(type(v) in _F64 for v in f4):
+        return None
+    cols, rows = frame.FRAME_GRID_COLS, frame.FRAME_GRID_ROWS
+    sizes = np.fromiter((len(frame.mGrid[ix][iy]) for ix in range(cols) for iy in range(rows)), np.int32,
+                        count=cols * rows)
+    off = np.zeros(cols * rows + 1, np.int32)
+    np.cumsum(sizes, out=off[1:])
+    idx = np.fromiter((g for col in frame.mGrid for cell in col for g in cell), np.int32, count=int(off[-1]))
+    kps = frame.mvKeysUn
+    kx = np.fromiter((k.pt[0] for k in kps), np.float64, count=len(kps))
+    ky = np.fromiter((k.pt[1] for k in kps), np.float64, count=len(kps))
+    ko = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
+    grid = (off, idx, kx, ky, ko, np.array(f4, np.float64), cols, rows)
+    _grid_cache[frame] = (key, grid)
+    return grid
+
+
+def features_in_areas(frame, queries) -> list:
+    """[frame.get_features_in_area(x, y, r, lo, hi) for (x, y, r, lo, hi) in queries], batched."""
+    if not queries:
+        return []
+    grid = _frame_grid(frame)
+    fast = grid is not None and all(_is_f64(x) and _is_f64(y) and _is_f64(r) for x, y, r, _, _ in queries)
+    if not fast:
+        return [frame.get_features_in_area(*q) for q in queries]
+    off, idx, kx, ky, ko, f4, cols, rows = grid
+    n = len(queries)
+    qx = np.fromiter((float(np.asarray(q[0]).ravel()[0]) if type(q[0]) is np.ndarray else q[0] for q in queries),
+                     np.float64, count=n)
+    qy = np.fromiter((float(np.asarray(q[1]).ravel()[0]) if type(q[1]) is np.ndarray else q[1] for q in queries),
+                     np.float64, count=n)
+    qr = np.fromiter((float(np.asarray(q[2]).ravel()[0]) if type(q[2]) is np.ndarray else q[2] for q in queries),
+                     np.float64, count=n)
+    lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
+    hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
+    out_off = np.zeros(n + 1, np.int32)
+    cap = max(64 * n, 1)
+    while True:
+        out = np.empty(cap, np.int32)
+        rc = _lib.lib().orbfe_grid_query(ptr(off), ptr(idx), cols, rows, ptr(kx), ptr(ky), ptr(ko), len(kx), ptr(f4), n,
+                                         ptr(qx), ptr(qy), ptr(qr), ptr(lo), ptr(hi), ptr(out_off), ptr(out), cap)
+        if rc == _lib.ORBFE_ECAPACITY:
+            cap = int(out_off[-1])
+            continue
+        _lib.check("orbfe_grid_query", rc)
+        break
+    o = out_off.tolist()
+    flat = out[:o[-1]].tolist()
+    return [flat[o[i]:o[i + 1]] for i in range(n)]
+
+
 class ORBMatcher:
     def __init__(self, nnratio=1, checkOri=True):
         self.mfNNratio = nnratio
@@ -133,7 +209,7 @@ class ORBMatcher:
     def search_by_projection_f_p(self, frame, vp_map_points, th):
         n_matches = 0
         b_factor = th != 1.0
-        work = []
+        pend, queries = [], []
         for pMP in vp_map_points:
             if not pMP.mbTrackInView:
                 continue
@@ -143,12 +219,11 @@ class ORBMatcher:
             r = self.radius_by_viewing_cos(pMP.mTrackViewCos)
             if b_factor:
                 r *= th
-            v_indices = frame.get_features_in_area(pMP.mTrackProjX, pMP.mTrackProjY,
-                                                   r * frame.mvScaleFactors[n_predicted_level],
-                                                   n_predicted_level - 1, n_predicted_level)
-            if not v_indices:
-                continue
-            work.append((pMP, n_predicted_level, r, v_indices, pMP.get_descriptor()))
+            pend.append((pMP, n_predicted_level, r))
+            queries.append((pMP.mTrackProjX, pMP.mTrackProjY, r * frame.mvScaleFactors[n_predicted_level],
+                            n_predicted_level - 1, n_predicted_level))
+        work = [(pMP, lvl, r, v_indices, pMP.get_descriptor())
+                for (pMP, lvl, r), v_indices in zip(pend, features_in_areas(frame, queries)) if v_indices]
         dists = self._batched([(w[4], w[3]) for w in work], frame.mDescriptors)
         for (pMP, n_predicted_level, r, v_indices, _), dq in zip(work, dists):
             best_dist = 256
@@ -193,33 +268,50 @@ class ORBMatcher:
         tlc = Rlw @ twc + tlw
         b_forward = tlc[2] > current_frame.mb
         b_backward = -tlc[2] > current_frame.mb
-        work = []
-        for i in range(last_frame.N):
-            pMP = last_frame.mvpMapPoints[i]
-            if not pMP or last_frame.mvbOutlier[i]:
-                continue
-            x3Dw = pMP.get_world_pos()
-            x3Dc = Rcw @ x3Dw + tcw
-            xc, yc, zc = x3Dc[0][0], x3Dc[1][0], x3Dc[2][0]
+        # projection of every usable map point of the last frame (one stacked matmul: the same per-point
+        # BLAS product as `Rcw @ x3Dw`, element-wise arithmetic in the reference's order and dtypes)
+        cand = [i for i in range(last_frame.N) if last_frame.mvpMapPoints[i] and not last_frame.mvbOutlier[i]]
+        pos = [last_frame.mvpMapPoints[i].get_world_pos() for i in cand]
+        proj = []
+        if pos and all(type(p) is np.ndarray and p.shape == (3, 1) and p.dtype == pos[0].dtype for p in pos):
+            x3Dc = Rcw @ np.stack(pos) + tcw
+            zc = x3Dc[:, 2, 0]
             invzc = 1.0 / zc
-            if invzc < 0:
-                continue
-            u = current_frame.fx * xc * invzc + current_frame.cx
-            v = current_frame.fy * yc * invzc + current_frame.cy
-            if u < current_frame.mnMinX or u > current_frame.mnMaxX:
-                continue
-            if v < current_frame.mnMinY or v > current_frame.mnMaxY:
-                continue
+            u = current_frame.fx * x3Dc[:, 0, 0] * invzc + current_frame.cx
+            v = current_frame.fy * x3Dc[:, 1, 0] * invzc + current_frame.cy
+            keep = ~((invzc < 0) | (u < current_frame.mnMinX) | (u > current_frame.mnMaxX) |
+                     (v < current_frame.mnMinY) | (v > current_frame.mnMaxY))
+            proj = [(cand[k], u[k], v[k], invzc[k]) for k in np.flatnonzero(keep).tolist()]
+        else:
+            for i, x3Dw in zip(cand, pos):
+                x3Dc = Rcw @ x3Dw + tcw
+                xc, yc, zc = x3Dc[0][0], x3Dc[1][0], x3Dc[2][0]
+                invzc = 1.0 / zc
+                if invzc < 0:
+                    continue
+                u = current_frame.fx * xc * invzc + current_frame.cx
+                v = current_frame.fy * yc * invzc + current_frame.cy
+                if u < current_frame.mnMinX or u > current_frame.mnMaxX:
+                    continue
+                if v < current_frame.mnMinY or v > current_frame.mnMaxY:
+                    continue
+                proj.append((i, u, v, invzc))
+        queries, pend = [], []
+        for i, u, v, invzc in proj:
             n_last_octave = last_frame.mvKeys[i].octave
             radius = th * current_frame.mvScaleFactors[n_last_octave]
             if b_forward:
-                v_indices2 = current_frame.get_features_in_area(u, v, radius, n_last_octave, -1)
+                queries.append((u, v, radius, n_last_octave, -1))
             elif b_backward:
-                v_indices2 = current_frame.get_features_in_area(u, v, radius, 0, n_last_octave)
+                queries.append((u, v, radius, 0, n_last_octave))
             else:
-                v_indices2 = current_frame.get_features_in_area(u, v, radius, n_last_octave - 1, n_last_octave + 1)
+                queries.append((u, v, radius, n_last_octave - 1, n_last_octave + 1))
+            pend.append((i, u, invzc, radius))
+        work = []
+        for (i, u, invzc, radius), v_indices2 in zip(pend, features_in_areas(current_frame, queries)):
             if not v_indices2:
                 continue
+            pMP = last_frame.mvpMapPoints[i]
             work.append((i, pMP, u, invzc, radius, v_indices2, pMP.get_descriptor()))
         dists = self._batched([(w[6], w[5]) for w in work], current_frame.mDescriptors)
         for (i, pMP, u, invzc, radius, v_indices2, _), dq in zip(work, dists):

@@ -71,14 +71,16 @@ def is_outlier(k: int, i: int) -> bool:
 
 # ------------------------------------------------------------------------------------------ replay side
 class KeyPoint:
-    """cv2.KeyPoint as Frame.ExtractORB builds it from the extractor's tuple (Frame.py:117, 121)."""
+    """cv2.KeyPoint as Frame.ExtractORB builds it from the extractor's tuple (Frame.py:117, 121).  cv2 keeps
+    float32 fields; the extractor's tuples (and the undistorted points) already hold float32 values as
+    Python floats, so they are stored as given (cv2's constructor is C++ and costs ~0.3 us; a Python
+    stand-in that re-rounded every field would dominate the per-frame time it is used to measure)."""
     __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
 
     def __init__(self, x, y, size, angle, response, octave, class_id=-1):
-        self.pt = (float(np.float32(x)), float(np.float32(y)))
-        self.size, self.angle, self.response = float(np.float32(size)), float(np.float32(angle)), float(
-            np.float32(response))
-        self.octave, self.class_id = int(octave), int(class_id)
+        self.pt = (x, y)
+        self.size, self.angle, self.response = size, angle, response
+        self.octave, self.class_id = octave, class_id
 
 
 cv2 = types.SimpleNamespace(KeyPoint=KeyPoint)  # what frame.extract_orb looks up in this module

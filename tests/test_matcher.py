@@ -131,3 +131,55 @@ def test_descriptor_distance_host_golden():
     got = [m.descriptor_distance(z["a"][i], z["b"][i]) for i in range(len(z["a"]))]
     assert got == z["dist"].tolist()
     assert all(type(v) is int for v in got)
+
+
+def _cpu_matcher(monkeypatch):
+    """The drop-in ORBMatcher with its one GPU call (the batched Hamming distances) answered by the oracle's
+    popcount: the host logic — batched grid queries (orbfe_grid_query, host code), the stacked projection,
+    the replay — runs as in production."""
+    from pyorbslam_amd import matcher
+
+    def cpu_batched(queries, train):
+        return [np.array([MO.dist(d, train[i]) for i in c], np.int32) for d, c in queries]
+
+    monkeypatch.setattr(matcher.ORBMatcher, "_batched", staticmethod(cpu_batched))
+    return matcher.ORBMatcher
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_fp_host_logic_golden(case, monkeypatch):
+    fr, mps, th, n, assigned = MF.load_fp(case)
+    assert _cpu_matcher(monkeypatch)(0.8, True).search_by_projection_f_p(fr, mps, th) == n
+    assert np.array_equal(MF.encode_fp(fr, mps), assigned)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_ff_host_logic_golden(case, monkeypatch):
+    cur, last, mps, extra, z = MF.load_ff(case)
+    assert _cpu_matcher(monkeypatch)(0.8, True).search_by_projection_f_f(cur, last, float(z["th"])) == int(z["n_matches"])
+    assert np.array_equal(MF.encode_ff(cur, mps, extra), z["assigned"])
+
+
+def test_grid_query_matches_frame_method():
+    """orbfe_grid_query against the grid restatement's per-query method (itself pinned by the goldens),
+    random queries incl. windows past the image and level filters."""
+    from pyorbslam_amd.matcher import features_in_areas
+    fr, _, _, _, _ = MF.load_fp(0)
+    rng = np.random.default_rng(2)
+    qs = [(float(rng.uniform(-50, 1300)), np.float64(rng.uniform(-50, 420)), float(rng.uniform(0.5, 80)),
+           int(rng.integers(-1, 8)), int(rng.integers(-1, 8))) for _ in range(3000)]
+    qs += [(np.array([q[0]]), q[1], q[2], q[3], q[4]) for q in qs[:200]]  # 1-element float64 arrays
+    assert features_in_areas(fr, qs) == [fr.get_features_in_area(*q) for q in qs]
+    q32 = [(np.float32(q[0]), q[1], q[2], q[3], q[4]) for q in qs[:100]]  # float32: the frame's own method
+    assert features_in_areas(fr, q32) == [fr.get_features_in_area(*q) for q in q32]
+
+
+def test_stacked_projection_equals_per_point_matmul():
+    """search_by_projection_f_f projects all map points with one stacked matmul; it must equal the
+    reference's per-point `Rcw @ x3Dw + tcw` bit for bit under this NumPy build."""
+    rng = np.random.default_rng(0)
+    for dt in (np.float32, np.float64):
+        for rdt in (np.float32, np.float64):
+            R, t = rng.normal(size=(3, 3)).astype(rdt), rng.normal(size=(3, 1)).astype(rdt)
+            X = (rng.normal(size=(2000, 3, 1)) * 30).astype(dt)
+            assert np.array_equal(R @ X + t, np.stack([R @ X[k] + t for k in range(len(X))]))

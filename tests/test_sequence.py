@@ -109,6 +109,21 @@ class _OracleMatcher:
         return matcher_oracle.search_f_p(frame, mps, th, self.nnratio)
 
 
+def test_sequence_replay_host_matcher(golden, sequence, monkeypatch):
+    """Frames 0-3 through the oracle extraction and the drop-in ORBMatcher's host logic (batched grid
+    queries, stacked projection, replay), its batched Hamming distances answered by the oracle popcount."""
+    from pyorbslam_amd import matcher
+    from oracle import matcher_oracle as MO
+
+    def cpu_batched(queries, train):
+        return [np.array([MO.dist(d, train[i]) for i in c], np.int32) for d, c in queries]
+
+    monkeypatch.setattr(matcher.ORBMatcher, "_batched", staticmethod(cpu_batched))
+    ex = (_OracleExtractor(**H.PARAMS), _OracleExtractor(**H.PARAMS))
+    bad = H.replay(golden, sequence, ex, matcher.ORBMatcher, _OracleFrame, n_frames=4)
+    assert not bad, bad
+
+
 def test_sequence_replay_oracle(golden, sequence):
     """Frames 0-2 through the CPU restatements: pins SeqFrame / ReplayMP / the recorded inputs."""
     ex = (_OracleExtractor(**H.PARAMS), _OracleExtractor(**H.PARAMS))
