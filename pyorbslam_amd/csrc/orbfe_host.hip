@@ -118,6 +118,7 @@ struct orbfe_ctx {
     DevBuf<uint8_t> d_shear;
     DevBuf<float> d_uin, d_uout;  // orbfe_undistort_points scratch
     HostBuf<uint8_t> h_frame;
+    HostBuf<uint8_t> h_in;  // pinned staging of host images (a pageable 2-D copy goes row by row)
     int64_t frame_pitch = 0;
     bool have_frame = false, frame_pyr = false;
     size_t fo_count = 0, fo_kps = 0, fo_desc = 0, fo_uR = 0, fo_depth = 0, fo_status = 0, fo_match = 0, fo_ovf = 0,
@@ -662,6 +663,23 @@ hipStream_t own(orbfe_ctx& c) {
     return c.own_stream;
 }
 
+// Host image rows -> the pinned staging buffer (one CPU pass), then ONE contiguous host->device copy on s.
+// A hipMemcpy2DAsync straight from pageable memory is staged by the runtime row by row: 6.8 ms per pair
+// of 1241x376 images, against 0.4 ms for the whole pair call this way (r2, tools/dbg/frame_extract_time.py).  The caller synchronises s before h_in is reused.
+void stage_images(orbfe_ctx& c, uint8_t* dst, const uint8_t* const* imgs, int n, int width, int height,
+                  int64_t stride, int64_t pitch, hipStream_t s) {
+    c.h_in.ensure((size_t)pitch * n);
+    for (int i = 0; i < n; ++i) {
+        uint8_t* o = c.h_in.p + (int64_t)i * pitch;
+        if (stride == width) {
+            std::memcpy(o, imgs[i], (size_t)width * height);
+        } else {
+            for (int y = 0; y < height; ++y) std::memcpy(o + (int64_t)y * width, imgs[i] + y * stride, width);
+        }
+    }
+    HIPCK(hipMemcpyAsync(dst, c.h_in.p, (size_t)pitch * (n - 1) + (size_t)width * height, hipMemcpyHostToDevice, s));
+}
+
 void check_overflow(orbfe_ctx& c) {
     int ovf = 0;
     HIPCK(hipMemcpy(&ovf, c.d_overflow.p, sizeof(int), hipMemcpyDeviceToHost));
@@ -727,7 +745,7 @@ int orbfe_extract(orbfe_handle h, const uint8_t* img, int32_t width, int32_t hei
         hipStream_t s = own(*h);
         const size_t bytes = (size_t)width * height;
         h->d_in.ensure(bytes);
-        HIPCK(hipMemcpy2DAsync(h->d_in.p, width, img, stride, width, height, hipMemcpyHostToDevice, s));
+        stage_images(*h, h->d_in.p, &img, 1, width, height, stride, (int64_t)bytes, s);
         enqueue_extract(*h, h->d_in.p, (int64_t)bytes, 1, s);
         int n = 0;
         HIPCK(hipMemcpyAsync(&n, h->d_count.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -802,8 +820,8 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
         hipStream_t s = own(*h);
         const int64_t pitch = ((int64_t)width * height + 255) & ~(int64_t)255;
         h->d_in.ensure(2 * (size_t)pitch);
-        HIPCK(hipMemcpy2DAsync(h->d_in.p, width, left, stride, width, height, hipMemcpyHostToDevice, s));
-        HIPCK(hipMemcpy2DAsync(h->d_in.p + pitch, width, right, stride, width, height, hipMemcpyHostToDevice, s));
+        const uint8_t* pair[2] = {left, right};
+        stage_images(*h, h->d_in.p, pair, 2, width, height, stride, pitch, s);
         HIPCK(hipMemsetAsync(h->d_overflow.p, 0, sizeof(int), s));
         extract_range(*h, h->d_in.p, pitch, 0, 2, s, false, false);
         stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, s);

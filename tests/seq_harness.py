@@ -22,6 +22,7 @@ the goldens were made with the reference's own methods, so matching them pins th
 """
 from __future__ import annotations
 
+import gc
 import hashlib
 import json
 import time
@@ -280,6 +281,10 @@ def replay(g: dict, sequence, extractors, matcher_cls, frame_cls, n_frames: int 
 
     for k in range(n_frames):
         p = f"f{k}_"
+        if timer is not None:
+            # collect the harness's own garbage (recorded projections, replaced map-point lists) between
+            # frames, outside the timed sections, so a cyclic-GC pass does not land inside one
+            gc.collect()
         L, R = sequence.frame(k)
         if sha(L) != str(g[p + "left_sha"]) or sha(R) != str(g[p + "right_sha"]):
             bad.append(f"frame {k}: synthetic images differ from the golden's")
