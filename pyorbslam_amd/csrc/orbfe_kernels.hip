@@ -480,12 +480,16 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         // ---- 2. pre-test, two adjacent pairs (pixels x .. x + 3) per lane and step, quads in row-major
         //         order (lane -> quad i0 + lane); the pair queue stays row-major (two ballots per step)
         const int qrow = (ww + 3) >> 2, nquad = qrow * wh;
-        const int step_y = 64 / qrow, step_x = 64 - step_y * qrow;
+        // n / qrow for n <= 64 without an integer division: (n + 0.5) / qrow is >= 0.5 / qrow >= 1/28 away
+        // from an integer, far more than the reciprocal's error
+        const float rq = __builtin_amdgcn_rcpf((float)qrow);
+        auto div_q = [&](int n) { return (int)__builtin_fmaf((float)n, rq, 0.5f * rq); };
+        const int step_y = div_q(64), step_x = 64 - step_y * qrow;
         int npq = 0;
         {
             // two 64-quad steps per iteration: both steps' ROI reads are issued before either waits
             // (one LDS round trip per 128 quads); lanes past the window read a clamped row and vote 0
-            int qy = lane / qrow, qx = lane - (lane / qrow) * qrow;
+            int qy = div_q(lane), qx = lane - qy * qrow;
             auto advance = [&](int& y, int& x) {
                 y += step_y;
                 x += step_x;
@@ -538,8 +542,9 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             if (k0 + 64 + lane < npq) e_next = pq[k0 + 64 + lane];
             if (k0 + lane < npq) {
                 const int x = e & 63, y = e >> 6;
-                uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
-                if (x + 1 >= ww) m = (m & 0xFFFFu) | 0x3C000000u;  // odd width: the pair's second pixel is border
+                // odd width: the last pair's second pixel lies outside the window; its map entry is cleared
+                // after this stage
+                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
                 // the u8 map keeps M itself (low byte of each biased half)
                 *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
                 h0 = (int)(m & 0x3FFu) > tlow;
@@ -552,6 +557,9 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             if (h) pq[nnq + lanes_below(bh)] = (uint16_t)e;
             nnq += __popcll(bh);
         }
+        // odd width: column ww (right of the window) got the outside pixel's M from the last pairs; NMS
+        // reads it as a neighbour (and as that pixel's own score) and needs 0 there
+        if ((ww & 1) && lane < wh) mm[(lane + 1) * MP + ww + 2] = 0;
         __syncthreads();
         if (V == 3) {  // ablation: + exact M
             if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
