@@ -1629,6 +1629,13 @@ constexpr int kStageItems = kSrcRows * 3;
 constexpr int kOrbHItems = 3;          // horizontal items per lane (189 of 192 used)
 constexpr int kOrbCSlots = 4;          // centroid slots per lane (213 of 256 used)
 
+// v_writelane_b32: lane `lane` (wave-uniform) of `old` becomes the uniform `v` (no builtin in this clang)
+// (gfx9 constant-bus rule: with an SGPR value the lane select goes through M0)
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v, int lane) {
+    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(v), "s"(lane) : "m0");
+    return old;
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1819,8 +1826,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                     h[rr][3] = __builtin_amdgcn_udot4(d2, w4(48, 34, 18, 0),
                                                       __builtin_amdgcn_udot4(d1, w4(18, 34, 48, 56), 0u, false), false);
                 }
-                *(uint4*)(hb + 4 * (hit[k] >> 16)) = uint4{h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
-                                                          h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
+                // (row 2p, row 2p + 1) as u16 pairs: one v_perm each (the sums are < 2^16)
+                auto pk = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
+                *(uint4*)(hb + 4 * (hit[k] >> 16)) = uint4{pk(h[0][0], h[1][0]), pk(h[0][1], h[1][1]),
+                                                          pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
             }
         }
         // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15)
@@ -1843,7 +1852,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         //      (H rows o .. o + 6), column c = col + 21; rint by the 1.5 * 2^23 trick (low mantissa bits
         //      hold 0x400000 + rint(x))
         const uint32_t cbase = 21u - __float_as_uint(12582912.0f);
-        uint64_t mine = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
+        uint32_t mine_lo = 0, mine_hi = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
 #pragma unroll 1
         for (int i = 0; i < 4; ++i) {
             const float4 pt = s_pat[lane + 64 * i];
@@ -1854,7 +1863,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 const df2 mm = (df2){py, py} * (df2){a, -b};
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
                 const uint32_t o = (__float_as_uint(rc.x) & 0xFFFFFFu) - 0x400000u + 18u;
-                const uint32_t c = __float_as_uint(rc.y) + cbase;
+                // c < 64: the mask lets the compiler put the four row offsets into the ds_read offsets
+                const uint32_t c = (__float_as_uint(rc.y) + cbase) & 63u;
                 const uint32_t* p = hb + (o >> 1) * kHDw + c;
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
                 const bool odd = o & 1u;
@@ -1865,10 +1875,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 v2[e] = s >> 16;
             }
             const uint64_t bb = __ballot(v2[0] < v2[1]);
-            mine = lane == i ? bb : mine;
+            mine_lo = writelane(mine_lo, (uint32_t)bb, i);  // lane i keeps this ballot
+            mine_hi = writelane(mine_hi, (uint32_t)(bb >> 32), i);
         }
         const int o = pre[l] + k0 + j;
-        if (lane < 4) *(uint64_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 8 * lane) = mine;
+        if (lane < 4) *(uint2*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 8 * lane) = uint2{mine_lo, mine_hi};
         if (lane == 0) {
             orbfe_keypoint kp;
             kp.x = l ? __fmul_rn((float)ccx, L.scale) : (float)ccx;
