@@ -250,6 +250,22 @@ int orbfe_grid_query(const int32_t* cell_off, const int32_t* cell_idx, int32_t c
                      const double* qx, const double* qy, const double* qr, const int32_t* qmin, const int32_t* qmax,
                      int32_t* out_off, int32_t* out_idx, int64_t cap);
 
+/* The sequential candidate selection of the tracking searches over precomputed distances (host code), for
+ * the ORBMatcher drop-in's double-typed fast path.  Queries are taken in order; query q's candidates are
+ * idx[off[q] .. off[q + 1]) with Hamming distances dist[...] (orbfe_hamming_csr); u_right = the frame's
+ * mvuRight as doubles (-1 for none); blocked[i] = 1 when frame slot i holds a map point with observations,
+ * updated in place with q_obs[q] when query q's map point takes slot best_idx[q] (-1: no match).
+ * orbfe_select_f_f: search_by_projection_f_f's inner loop and TH_HIGH test (ORBMatcher.py:348-372): stereo
+ * gate |(u - mbf * invzc) - uR| > radius in double.  orbfe_select_f_p: search_by_projection_f_p's
+ * (ORBMatcher.py:246-281): gate |xr - uR| > r_scaled, best / second best with their keypoint octaves and
+ * the ratio test best > nnratio * second when both are on one octave. */
+int orbfe_select_f_f(int32_t n_q, const int32_t* off, const int32_t* idx, const int32_t* dist, const double* u,
+                     const double* invzc, const double* radius, const uint8_t* q_obs, const double* u_right,
+                     uint8_t* blocked, int32_t n_frame, double mbf, int32_t th_high, int32_t* best_idx);
+int orbfe_select_f_p(int32_t n_q, const int32_t* off, const int32_t* idx, const int32_t* dist, const double* xr,
+                     const double* r_scaled, const int32_t* kp_octave, const uint8_t* q_obs, const double* u_right,
+                     uint8_t* blocked, int32_t n_frame, double nnratio, int32_t th_high, int32_t* best_idx);
+
 /* All-pairs Hamming distance matrix (n_a x n_b int32) — descriptor_distance batched. */
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out);

@@ -1162,6 +1162,83 @@ int orbfe_grid_query(const int32_t* cell_off, const int32_t* cell_idx, int32_t c
     });
 }
 
+// The sequential candidate selection of the two tracking searches over precomputed distances, in double
+// (this file is built with -ffp-contract=off: `u - mbf * invzc` stays two roundings like Python's).
+// blocked[i] = "slot i holds a map point with observations" (the `if mvpMapPoints[i]: if ...observations()
+// > 0: continue` test); a match stores the query's own flag there, as the reference's assignment changes
+// what later queries of the same search read.
+namespace {
+void check_select(int32_t n_q, const int32_t* off, const int32_t* idx, const int32_t* dist, const double* u_right,
+                  const uint8_t* blocked, int32_t n_frame, const int32_t* best_idx) {
+    if (n_q < 0 || n_frame < 0) throw Error(ORBFE_EINVAL, "negative size");
+    if (n_q > 0 && (!off || !best_idx)) throw Error(ORBFE_EINVAL, "null argument");
+    if (n_q > 0 && off[n_q] > 0 && (!idx || !dist || !u_right || !blocked)) throw Error(ORBFE_EINVAL, "null argument");
+    for (int32_t k = 0; n_q > 0 && k < off[n_q]; ++k)
+        if (idx[k] < 0 || idx[k] >= n_frame) throw Error(ORBFE_EINVAL, "candidate index out of range");
+}
+}  // namespace
+
+int orbfe_select_f_f(int32_t n_q, const int32_t* off, const int32_t* idx, const int32_t* dist, const double* u,
+                     const double* invzc, const double* radius, const uint8_t* q_obs, const double* u_right,
+                     uint8_t* blocked, int32_t n_frame, double mbf, int32_t th_high, int32_t* best_idx) {
+    return guarded([&] {
+        check_select(n_q, off, idx, dist, u_right, blocked, n_frame, best_idx);
+        for (int32_t q = 0; q < n_q; ++q) {
+            int best_dist = 256, best = -1;
+            for (int32_t k = off[q]; k < off[q + 1]; ++k) {  // ORBMatcher.py:348-368
+                const int i2 = idx[k];
+                if (blocked[i2]) continue;
+                if (u_right[i2] > 0) {
+                    const double ur = u[q] - mbf * invzc[q];
+                    if (std::fabs(ur - u_right[i2]) > radius[q]) continue;
+                }
+                if (dist[k] < best_dist) {
+                    best_dist = dist[k];
+                    best = i2;
+                }
+            }
+            if (best_dist <= th_high) {  // :370-372
+                best_idx[q] = best;
+                blocked[best] = q_obs[q];
+            } else {
+                best_idx[q] = -1;
+            }
+        }
+    });
+}
+
+int orbfe_select_f_p(int32_t n_q, const int32_t* off, const int32_t* idx, const int32_t* dist, const double* xr,
+                     const double* r_scaled, const int32_t* kp_octave, const uint8_t* q_obs, const double* u_right,
+                     uint8_t* blocked, int32_t n_frame, double nnratio, int32_t th_high, int32_t* best_idx) {
+    return guarded([&] {
+        check_select(n_q, off, idx, dist, u_right, blocked, n_frame, best_idx);
+        for (int32_t q = 0; q < n_q; ++q) {
+            int bd = 256, bl = -1, bd2 = 256, bl2 = -1, bi = -1;
+            for (int32_t k = off[q]; k < off[q + 1]; ++k) {  // ORBMatcher.py:246-275
+                const int i = idx[k];
+                if (blocked[i]) continue;
+                if (u_right[i] > 0 && std::fabs(xr[q] - u_right[i]) > r_scaled[q]) continue;
+                const int d = dist[k];
+                if (d < bd) {
+                    bd2 = bd;
+                    bd = d;
+                    bl2 = bl;
+                    bl = kp_octave[i];
+                    bi = i;
+                } else if (d < bd2) {
+                    bl2 = kp_octave[i];
+                    bd2 = d;
+                }
+            }
+            best_idx[q] = -1;
+            if (bd <= th_high && !(bl == bl2 && (double)bd > nnratio * (double)bd2)) {  // :276-281
+                best_idx[q] = bi;
+                blocked[bi] = q_obs[q];
+            }
+        }
+    });
+}
+
 int orbfe_hamming_matrix(orbfe_handle h, const uint8_t* a_desc, int32_t n_a, const uint8_t* b_desc, int32_t n_b,
                          int32_t* out) {
     return guarded([&] {

@@ -139,24 +139,12 @@ def _frame_grid(frame):
     return grid
 
 
-def features_in_areas(frame, queries) -> list:
-    """[frame.get_features_in_area(x, y, r, lo, hi) for (x, y, r, lo, hi) in queries], batched."""
-    if not queries:
-        return []
-    grid = _frame_grid(frame)
-    fast = grid is not None and all(_is_f64(x) and _is_f64(y) and _is_f64(r) for x, y, r, _, _ in queries)
-    if not fast:
-        return [frame.get_features_in_area(*q) for q in queries]
+def _grid_csr(frame, grid, qx, qy, qr, lo, hi):
+    """orbfe_grid_query over float64 / int32 query arrays: (out_off, out_idx) as int32 arrays."""
     off, idx, kx, ky, ko, f4, cols, rows = grid
-    n = len(queries)
-    qx = np.fromiter((float(np.asarray(q[0]).ravel()[0]) if type(q[0]) is np.ndarray else q[0] for q in queries),
-                     np.float64, count=n)
-    qy = np.fromiter((float(np.asarray(q[1]).ravel()[0]) if type(q[1]) is np.ndarray else q[1] for q in queries),
-                     np.float64, count=n)
-    qr = np.fromiter((float(np.asarray(q[2]).ravel()[0]) if type(q[2]) is np.ndarray else q[2] for q in queries),
-                     np.float64, count=n)
-    lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
-    hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
+    qx, qy, qr = (np.ascontiguousarray(a, np.float64) for a in (qx, qy, qr))
+    lo, hi = np.ascontiguousarray(lo, np.int32), np.ascontiguousarray(hi, np.int32)
+    n = len(qx)
     out_off = np.zeros(n + 1, np.int32)
     cap = max(64 * n, 1)
     while True:
@@ -167,10 +155,63 @@ def features_in_areas(frame, queries) -> list:
             cap = int(out_off[-1])
             continue
         _lib.check("orbfe_grid_query", rc)
-        break
+        return out_off, out[:int(out_off[-1])]
+
+
+def features_in_areas(frame, queries) -> list:
+    """[frame.get_features_in_area(x, y, r, lo, hi) for (x, y, r, lo, hi) in queries], batched."""
+    if not queries:
+        return []
+    grid = _frame_grid(frame)
+    fast = grid is not None and all(_is_f64(x) and _is_f64(y) and _is_f64(r) for x, y, r, _, _ in queries)
+    if not fast:
+        return [frame.get_features_in_area(*q) for q in queries]
+    n = len(queries)
+    qx = np.fromiter((float(np.asarray(q[0]).ravel()[0]) if type(q[0]) is np.ndarray else q[0] for q in queries),
+                     np.float64, count=n)
+    qy = np.fromiter((float(np.asarray(q[1]).ravel()[0]) if type(q[1]) is np.ndarray else q[1] for q in queries),
+                     np.float64, count=n)
+    qr = np.fromiter((float(np.asarray(q[2]).ravel()[0]) if type(q[2]) is np.ndarray else q[2] for q in queries),
+                     np.float64, count=n)
+    lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
+    hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
+    out_off, out = _grid_csr(frame, grid, qx, qy, qr, lo, hi)
     o = out_off.tolist()
-    flat = out[:o[-1]].tolist()
+    flat = out.tolist()
     return [flat[o[i]:o[i + 1]] for i in range(n)]
+
+
+# Per-frame inputs of the native candidate selection: mvuRight as doubles (set once by the Frame
+# constructor), and which slots hold a map point with observations (read fresh per search).
+_uright_cache = weakref.WeakKeyDictionary()
+
+
+def _u_right(frame):
+    vals = frame.mvuRight
+    try:
+        ent = _uright_cache.get(frame)
+    except TypeError:
+        ent = None
+    if ent is not None and ent[0] == (id(vals), len(vals)):
+        return ent[1]
+    arr = np.fromiter((float(v) for v in vals), np.float64, count=len(vals))
+    try:
+        _uright_cache[frame] = ((id(vals), len(vals)), arr)
+    except TypeError:
+        pass
+    return arr
+
+
+def _blocked(frame):
+    mps = frame.mvpMapPoints
+    if mps.count(None) == len(mps):
+        return np.zeros(len(mps), np.uint8)
+    return np.fromiter((1 if (m is not None and m and m.observations() > 0) else 0 for m in mps), np.uint8,
+                       count=len(mps))
+
+
+def _obs_flags(mps) -> np.ndarray:
+    return np.fromiter((1 if (m and m.observations() > 0) else 0 for m in mps), np.uint8, count=len(mps))
 
 
 class ORBMatcher:
@@ -193,7 +234,12 @@ class ORBMatcher:
         return 2.5 if view_cos > 0.998 else 4.0
 
     @staticmethod
-    def _batched(queries, train):
+    def _csr(qd, train, off, idx):
+        """The one device call of a search: distances of CSR (query, candidate) pairs."""
+        return hamming_csr(qd, train, off, idx)
+
+    @classmethod
+    def _batched(cls, queries, train):
         """queries: list of (descriptor, candidate list) -> list of distance arrays."""
         off = np.zeros(len(queries) + 1, np.int32)
         for i, (_, c) in enumerate(queries):
@@ -202,8 +248,20 @@ class ORBMatcher:
             return [np.zeros(0, np.int32) for _ in queries]
         qd = np.stack([np.asarray(d, np.uint8).reshape(32) for d, _ in queries])
         idx = np.concatenate([np.asarray(c, np.int32) for _, c in queries])
-        dist = hamming_csr(qd, train, off, idx)
+        dist = cls._csr(qd, train, off, idx)
         return [dist[off[i]:off[i + 1]] for i in range(len(queries))]
+
+    def _nonempty(self, off, idx, pmps, train):
+        """Restrict a CSR candidate set to its non-empty queries and get their distances: (rows, off, dist),
+        rows = indices of the non-empty queries (the reference fetches a descriptor only for those)."""
+        cnt = np.diff(off)
+        rows = np.flatnonzero(cnt)
+        off2 = np.zeros(len(rows) + 1, np.int32)
+        np.cumsum(cnt[rows], out=off2[1:])
+        if len(rows) == 0:
+            return rows, off2, np.zeros(0, np.int32)
+        qd = np.stack([np.asarray(pmps[r].get_descriptor(), np.uint8).reshape(32) for r in rows.tolist()])
+        return rows, off2, np.ascontiguousarray(self._csr(qd, train, off2, idx), np.int32)
 
     # ORBMatcher.py:215-283
     def search_by_projection_f_p(self, frame, vp_map_points, th):
@@ -222,6 +280,9 @@ class ORBMatcher:
             pend.append((pMP, n_predicted_level, r))
             queries.append((pMP.mTrackProjX, pMP.mTrackProjY, r * frame.mvScaleFactors[n_predicted_level],
                             n_predicted_level - 1, n_predicted_level))
+        done = self._f_p_native(frame, pend, queries)
+        if done is not None:
+            return done
         work = [(pMP, lvl, r, v_indices, pMP.get_descriptor())
                 for (pMP, lvl, r), v_indices in zip(pend, features_in_areas(frame, queries)) if v_indices]
         dists = self._batched([(w[4], w[3]) for w in work], frame.mDescriptors)
@@ -281,7 +342,11 @@ class ORBMatcher:
             v = current_frame.fy * x3Dc[:, 1, 0] * invzc + current_frame.cy
             keep = ~((invzc < 0) | (u < current_frame.mnMinX) | (u > current_frame.mnMaxX) |
                      (v < current_frame.mnMinY) | (v > current_frame.mnMaxY))
-            proj = [(cand[k], u[k], v[k], invzc[k]) for k in np.flatnonzero(keep).tolist()]
+            sel = np.flatnonzero(keep)
+            done = self._f_f_native(current_frame, last_frame, th, b_forward, b_backward, cand, sel, u, v, invzc)
+            if done is not None:
+                return done
+            proj = [(cand[k], u[k], v[k], invzc[k]) for k in sel.tolist()]
         else:
             for i, x3Dw in zip(cand, pos):
                 x3Dc = Rcw @ x3Dw + tcw
@@ -347,6 +412,111 @@ class ORBMatcher:
                 if i not in (ind1, ind2, ind3):
                     for idx in rot_hist[i]:
                         current_frame.mvpMapPoints[idx] = None
+                        n_matches -= 1
+        return n_matches
+
+    # ------------------------------------------------------------------------------------------------
+    # native selection of the two tracking searches (orbfe_select_f_p / _f_f, host code) when every value
+    # the reference's loop compares is a double: grid query -> distances of the non-empty queries -> the
+    # sequential selection in C -> the assignments (and f_f's rotation histogram) here, in order.  Returns
+    # None, before touching anything, when an operand has another type (float32 projections promote
+    # differently under NumPy 2): the caller then runs the Python loop.
+
+    def _f_p_native(self, frame, pend, queries):
+        grid = _frame_grid(frame)
+        if grid is None or not queries:
+            return None
+        if not all(_is_f64(x) and _is_f64(y) and _is_f64(r) for x, y, r, _, _ in queries):
+            return None
+        pmps = [p for p, _, _ in pend]
+        xr_all = [p.mTrackProjXR for p in pmps]
+        if not all(_is_f64(x) for x in xr_all):
+            return None
+        n_frame = len(frame.mvpMapPoints)
+        u_right = _u_right(frame)
+        if len(u_right) != n_frame or len(grid[4]) != n_frame:
+            return None
+        n = len(queries)
+        f64 = lambda v: float(np.asarray(v).ravel()[0]) if type(v) is np.ndarray else v  # noqa: E731
+        qx = np.fromiter((f64(q[0]) for q in queries), np.float64, count=n)
+        qy = np.fromiter((f64(q[1]) for q in queries), np.float64, count=n)
+        qr = np.fromiter((f64(q[2]) for q in queries), np.float64, count=n)
+        lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
+        hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
+        off, idx = _grid_csr(frame, grid, qx, qy, qr, lo, hi)
+        rows, off2, dist = self._nonempty(off, idx, pmps, frame.mDescriptors)
+        if len(rows) == 0:
+            return 0
+        rl = rows.tolist()
+        xr = np.fromiter((f64(xr_all[r]) for r in rl), np.float64, count=len(rl))
+        rs = np.ascontiguousarray(qr[rows])
+        q_obs = _obs_flags([pmps[r] for r in rl])
+        blocked = _blocked(frame)
+        best = np.empty(len(rl), np.int32)
+        call("orbfe_select_f_p", len(rl), ptr(off2), ptr(idx), ptr(dist), ptr(xr), ptr(rs), ptr(grid[4]), ptr(q_obs),
+             ptr(u_right), ptr(blocked), n_frame, float(self.mfNNratio), TH_HIGH, ptr(best))
+        n_matches = 0
+        for j in np.flatnonzero(best >= 0).tolist():
+            frame.mvpMapPoints[int(best[j])] = pmps[rl[j]]
+            n_matches += 1
+        return n_matches
+
+    def _f_f_native(self, cur, last, th, b_forward, b_backward, cand, sel, u, v, invzc):
+        grid = _frame_grid(cur)
+        if grid is None or type(th) not in (int, float):
+            return None
+        if not (u.dtype == np.float64 and v.dtype == np.float64 and invzc.dtype == np.float64):
+            return None
+        sf = cur.mvScaleFactors
+        if not all(type(x) in _F64 for x in sf):
+            return None
+        n_frame = len(cur.mvpMapPoints)
+        u_right = _u_right(cur)
+        if len(u_right) != n_frame:
+            return None
+        ci = np.asarray(cand, np.int64)[sel].tolist()
+        octv = np.fromiter((last.mvKeys[i].octave for i in ci), np.int32, count=len(ci))
+        radius = th * np.asarray(sf, np.float64)[octv]  # th * mvScaleFactors[octave], one double product each
+        if b_forward:
+            lo, hi = octv, np.full(len(ci), -1, np.int32)
+        elif b_backward:
+            lo, hi = np.zeros(len(ci), np.int32), octv
+        else:
+            lo, hi = octv - 1, octv + 1
+        qx, iz = np.ascontiguousarray(u[sel]), np.ascontiguousarray(invzc[sel])
+        off, idx = _grid_csr(cur, grid, qx, v[sel], radius, lo, hi)
+        pmps = [last.mvpMapPoints[i] for i in ci]
+        rows, off2, dist = self._nonempty(off, idx, pmps, cur.mDescriptors)
+        n_matches = 0
+        rot_hist = [[] for _ in range(HISTO_LENGTH)]
+        factor = 1.0 / HISTO_LENGTH
+        if len(rows):
+            rl = rows.tolist()
+            q_obs = _obs_flags([pmps[r] for r in rl])
+            blocked = _blocked(cur)
+            best = np.empty(len(rl), np.int32)
+            qu, qz, qrad = (np.ascontiguousarray(a[rows], np.float64) for a in (qx, iz, radius))  # held across the call
+            call("orbfe_select_f_f", len(rl), ptr(off2), ptr(idx), ptr(dist), ptr(qu), ptr(qz), ptr(qrad), ptr(q_obs),
+                 ptr(u_right), ptr(blocked), n_frame, float(cur.mbf), TH_HIGH, ptr(best))
+            for j in np.flatnonzero(best >= 0).tolist():
+                b = int(best[j])
+                cur.mvpMapPoints[b] = pmps[rl[j]]
+                n_matches += 1
+                if self.mbCheckOrientation:  # ORBMatcher.py:374-382
+                    rot = last.mvKeysUn[ci[rl[j]]].angle - cur.mvKeysUn[b].angle
+                    if rot < 0.0:
+                        rot += 360.0
+                    bin_idx = round(rot * factor)
+                    if bin_idx == HISTO_LENGTH:
+                        bin_idx = 0
+                    assert 0 <= bin_idx < HISTO_LENGTH
+                    rot_hist[bin_idx].append(b)
+        if self.mbCheckOrientation:
+            ind1, ind2, ind3 = self.compute_three_maxima(rot_hist, HISTO_LENGTH)
+            for i in range(HISTO_LENGTH):
+                if i not in (ind1, ind2, ind3):
+                    for idx2 in rot_hist[i]:
+                        cur.mvpMapPoints[idx2] = None
                         n_matches -= 1
         return n_matches
 

@@ -133,30 +133,42 @@ def test_descriptor_distance_host_golden():
     assert all(type(v) is int for v in got)
 
 
-def _cpu_matcher(monkeypatch):
-    """The drop-in ORBMatcher with its one GPU call (the batched Hamming distances) answered by the oracle's
-    popcount: the host logic — batched grid queries (orbfe_grid_query, host code), the stacked projection,
-    the replay — runs as in production."""
+def cpu_csr(qd, train, off, idx):
+    """orbfe_hamming_csr on the host (numpy popcount): the one GPU call of the matcher searches."""
+    q = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    t = np.asarray(train, np.uint8).reshape(-1, 32)
+    x = np.bitwise_xor(np.asarray(qd, np.uint8).reshape(-1, 32)[q], t[np.asarray(idx, np.int64)])
+    return np.unpackbits(x, axis=1).sum(1).astype(np.int32)
+
+
+def _cpu_matcher(monkeypatch, native=True):
+    """The drop-in ORBMatcher with its one GPU call (the batched Hamming distances) answered on the host:
+    the host logic — batched grid queries (orbfe_grid_query), the stacked projection, the native candidate
+    selection (orbfe_select_f_f / _f_p, host code) or, with native=False, the Python replay — runs as in
+    production."""
     from pyorbslam_amd import matcher
 
-    def cpu_batched(queries, train):
-        return [np.array([MO.dist(d, train[i]) for i in c], np.int32) for d, c in queries]
-
-    monkeypatch.setattr(matcher.ORBMatcher, "_batched", staticmethod(cpu_batched))
+    monkeypatch.setattr(matcher.ORBMatcher, "_csr", staticmethod(cpu_csr))
+    if not native:
+        monkeypatch.setattr(matcher.ORBMatcher, "_f_f_native", lambda self, *a: None)
+        monkeypatch.setattr(matcher.ORBMatcher, "_f_p_native", lambda self, *a: None)
     return matcher.ORBMatcher
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("case", range(6))
-def test_fp_host_logic_golden(case, monkeypatch):
+def test_fp_host_logic_golden(case, native, monkeypatch):
     fr, mps, th, n, assigned = MF.load_fp(case)
-    assert _cpu_matcher(monkeypatch)(0.8, True).search_by_projection_f_p(fr, mps, th) == n
+    assert _cpu_matcher(monkeypatch, native)(0.8, True).search_by_projection_f_p(fr, mps, th) == n
     assert np.array_equal(MF.encode_fp(fr, mps), assigned)
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("case", range(6))
-def test_ff_host_logic_golden(case, monkeypatch):
+def test_ff_host_logic_golden(case, native, monkeypatch):
     cur, last, mps, extra, z = MF.load_ff(case)
-    assert _cpu_matcher(monkeypatch)(0.8, True).search_by_projection_f_f(cur, last, float(z["th"])) == int(z["n_matches"])
+    m = _cpu_matcher(monkeypatch, native)(0.8, True)
+    assert m.search_by_projection_f_f(cur, last, float(z["th"])) == int(z["n_matches"])
     assert np.array_equal(MF.encode_ff(cur, mps, extra), z["assigned"])
 
 

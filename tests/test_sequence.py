@@ -115,13 +115,22 @@ def test_sequence_replay_host_matcher(golden, sequence, monkeypatch):
     from pyorbslam_amd import matcher
     from oracle import matcher_oracle as MO
 
-    def cpu_batched(queries, train):
-        return [np.array([MO.dist(d, train[i]) for i in c], np.int32) for d, c in queries]
+    from test_matcher import cpu_csr
 
-    monkeypatch.setattr(matcher.ORBMatcher, "_batched", staticmethod(cpu_batched))
+    monkeypatch.setattr(matcher.ORBMatcher, "_csr", staticmethod(cpu_csr))
+    taken = {"f_f": 0, "f_p": 0}
+    for name in ("f_f", "f_p"):
+        orig = getattr(matcher.ORBMatcher, f"_{name}_native")
+
+        def spy(self, *a, _orig=orig, _name=name):
+            r = _orig(self, *a)
+            taken[_name] += r is not None
+            return r
+        monkeypatch.setattr(matcher.ORBMatcher, f"_{name}_native", spy)
     ex = (_OracleExtractor(**H.PARAMS), _OracleExtractor(**H.PARAMS))
     bad = H.replay(golden, sequence, ex, matcher.ORBMatcher, _OracleFrame, n_frames=4)
     assert not bad, bad
+    assert taken["f_f"] >= 3 and taken["f_p"] >= 3, taken  # the tracking loop's doubles take the native selection
 
 
 def test_sequence_replay_oracle(golden, sequence):
