@@ -167,12 +167,9 @@ def features_in_areas(frame, queries) -> list:
     if not fast:
         return [frame.get_features_in_area(*q) for q in queries]
     n = len(queries)
-    qx = np.fromiter((float(np.asarray(q[0]).ravel()[0]) if type(q[0]) is np.ndarray else q[0] for q in queries),
-                     np.float64, count=n)
-    qy = np.fromiter((float(np.asarray(q[1]).ravel()[0]) if type(q[1]) is np.ndarray else q[1] for q in queries),
-                     np.float64, count=n)
-    qr = np.fromiter((float(np.asarray(q[2]).ravel()[0]) if type(q[2]) is np.ndarray else q[2] for q in queries),
-                     np.float64, count=n)
+    qx = np.fromiter((q[0].item() if type(q[0]) is np.ndarray else q[0] for q in queries), np.float64, count=n)
+    qy = np.fromiter((q[1].item() if type(q[1]) is np.ndarray else q[1] for q in queries), np.float64, count=n)
+    qr = np.fromiter((q[2].item() if type(q[2]) is np.ndarray else q[2] for q in queries), np.float64, count=n)
     lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
     hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
     out_off, out = _grid_csr(frame, grid, qx, qy, qr, lo, hi)
@@ -437,7 +434,7 @@ class ORBMatcher:
         if len(u_right) != n_frame or len(grid[4]) != n_frame:
             return None
         n = len(queries)
-        f64 = lambda v: float(np.asarray(v).ravel()[0]) if type(v) is np.ndarray else v  # noqa: E731
+        f64 = lambda v: v.item() if type(v) is np.ndarray else v  # noqa: E731  (size-1 float64: .item() is exact)
         qx = np.fromiter((f64(q[0]) for q in queries), np.float64, count=n)
         qy = np.fromiter((f64(q[1]) for q in queries), np.float64, count=n)
         qr = np.fromiter((f64(q[2]) for q in queries), np.float64, count=n)
