@@ -35,6 +35,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4  # wave64 VALU issue, all SIMDs at the 2.4 GHz peak clock
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 STAGES = ["resize", "detect", "octree", "blur", "describe", "stereo"]
 STAGE_KERNELS = {"resize": "k_resize (x7 levels)", "detect": "k_detect", "octree": "k_octree", "blur": "(fused in k_orb)",
@@ -442,6 +443,23 @@ def main():
             out["stage_roofline"] = {s: {"ms": round(stage_ms[s], 4), "achieved_GBs": round(ach[s], 3),
                                          "frac": round(ach[s] / HBM_PEAK_GBS, 6), "traffic": (tr or {}).get(s)}
                                      for s in ach}
+            # the bound these kernels actually meet: VALU issue (wave-instructions per step from
+            # SQ_INSTS_VALU over the same standalone pass, profiles/valu.json, tools/valu.py)
+            vf = ROOT / "profiles" / "valu.json"
+            vi = json.loads(vf.read_text()).get(workload + "_standalone") if vf.exists() else None
+            if vi:
+                vst = {s: vi[s] / (stage_ms[s] * 1e-3) / 1e9 for s in vi if stage_ms.get(s, 0) > 0}
+                vdom = max(vst, key=lambda s: stage_ms[s])
+                out["valu_roofline"] = {
+                    "bound": "valu", "unit": "G wave-instructions/s", "peak": VALU_PEAK_GIPS,
+                    "peak_def": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction",
+                    "kernel": STAGE_KERNELS[vdom], "achieved": round(vst[vdom], 2),
+                    "frac": round(vst[vdom] / VALU_PEAK_GIPS, 4),
+                    "stages": {s: {"inst_per_step": int(vi[s]), "achieved": round(v, 2),
+                                   "frac": round(v / VALU_PEAK_GIPS, 4)} for s, v in vst.items()},
+                    "pipeline_frac": (round(sum(vi.values()) * pairs_per_s / world / P / 1e9 / VALU_PEAK_GIPS, 4)
+                                      if pairs_per_s else None),
+                    "source": "profiles/valu.json " + workload + "_standalone (rocprofv3 --pmc SQ_INSTS_VALU)"}
         if gather is not None:
             out["with_gather"] = gather
         out["cpu_baseline"] = cpu

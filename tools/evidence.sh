@@ -3,7 +3,8 @@
 # workload + standalone per-stage roofline pass + cpu_baseline), the C3 frame-mode line, a gloo 2-rank
 # rehearsal with the timed device-side gather, a rocprofv3 kernel trace of the default bench command, and
 # FETCH_SIZE / WRITE_SIZE passes (one counter pass each, as MI355X_MICROARCH.md prescribes) over the
-# standalone pass only (--roofline-only) that profiles/traffic.json is built from.
+# standalone pass only (--roofline-only) that profiles/traffic.json is built from, and an SQ_INSTS_VALU pass
+# for profiles/valu.json (tools/valu.py).
 # usage (on the GPU box): bash tools/evidence.sh TAG      -> gpurun_out/ev_TAG/
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -29,4 +30,5 @@ step bench_gather2_gloo 300 env ORBFE_DIST_BACKEND=gloo python -m torch.distribu
 step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ktrace" -o run -- python bench.py --cpu-sample 0
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o run -- python bench.py --roofline-only --roofline-steps 2
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o run -- python bench.py --roofline-only --roofline-steps 2
+step pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc_valu" -o run -- python bench.py --roofline-only --roofline-steps 2
 echo "evidence done"
