@@ -411,12 +411,14 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
     xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
     const int lane = threadIdx.x;
     const int c_first = bx * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
-    // ROI staging, 16 lanes per row (dword d), 4 rows per step (NS steps): lane d loads dword d of the row
-    // from the 4-byte aligned start of column -1 and takes dword d + 1 from its neighbour lane (DPP
-    // row_shl:1) to re-align with v_alignbyte (rows are <= 59 px, so 16 dwords cover every row).  The
-    // loads of the next cell are issued before this cell's compute (prefetch into NS registers).
-    const int d = lane & 15, r0 = lane >> 4;
-    uint32_t raw[NS];
+    // ROI staging, 8 lanes per row (dwords 2d, 2d + 1), 8 rows per step (NS / 2 steps): lane d loads two
+    // dwords of the row from the 4-byte aligned start of column -1 and takes dword 2d + 2 from its
+    // neighbour lane (DPP row_shl:1) to re-align 8 bytes with v_alignbyte (rows are <= 59 px, so 16
+    // dwords cover every row; what lane 7 receives from the next row's lane only lands in columns >= 60).
+    // The loads of the next cell are issued before this cell's compute (prefetch into NS registers).
+    constexpr int NS2 = NS / 2;
+    const int d = lane & 7, r0 = lane >> 3;
+    uint2 raw[NS2];
     auto issue = [&](int c) {
         const CellGeo cg = load_cell(cells, c);
         int stride;
@@ -426,13 +428,13 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
         const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const int r = r0 + 4 * k;
-            raw[k] = 0u;
-            if (r < rh && d <= ndw) {
-                const uint32_t off = off0 + (uint32_t)(4 * k * stride);
+        for (int k = 0; k < NS2; ++k) {
+            const int r = r0 + 8 * k;
+            raw[k] = uint2{0u, 0u};
+            if (r < rh && 2 * d <= ndw) {
+                const uint32_t off = off0 + (uint32_t)(8 * k * stride);
                 const uint32_t al = off - ((lvl_lo + off) & 3u);
-                raw[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * d, 0, 0);
+                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al + 8u * d, 0, 0));
             }
         }
     };
@@ -446,19 +448,22 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
             const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
             const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
-            const int ndw = (rw + 4) >> 2;
+            const int n8 = (rw + 8) >> 3;  // 8-column groups of columns -1 .. rw-1 (8 * n8 <= RP)
 #pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                // every lane takes part in the DPP (uniform control flow); lanes 15 of a row get 0
-                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)raw[k], 0x101, 0xF, 0xF, false);
-                const int r = r0 + 4 * k;
-                if (r < rh && d < ndw) {
-                    const int sh = (int)((lvl_lo + off0 + (uint32_t)(4 * k * stride)) & 3u);
-                    const uint32_t w = __builtin_amdgcn_alignbyte(nb, raw[k], sh);
-                    uint2 u;
-                    u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04010400u);
-                    u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w, 0x04030402u);
-                    *(uint2*)(roi + r * RP + 4 * d) = u;
+            for (int k = 0; k < NS2; ++k) {
+                // every lane takes part in the DPP (uniform control flow); lanes 15 of a DPP row get 0
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)raw[k].x, 0x101, 0xF, 0xF, false);
+                const int r = r0 + 8 * k;
+                if (r < rh && d < n8) {
+                    const int sh = (int)((lvl_lo + off0 + (uint32_t)(8 * k * stride)) & 3u);
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(raw[k].y, raw[k].x, sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(nb, raw[k].y, sh);
+                    uint4 u;
+                    u.x = __builtin_amdgcn_perm(0x3C3C3C3Cu, w0, 0x04010400u);
+                    u.y = __builtin_amdgcn_perm(0x3C3C3C3Cu, w0, 0x04030402u);
+                    u.z = __builtin_amdgcn_perm(0x3C3C3C3Cu, w1, 0x04010400u);
+                    u.w = __builtin_amdgcn_perm(0x3C3C3C3Cu, w1, 0x04030402u);
+                    *(uint4*)(roi + r * RP + 8 * d) = u;
                 }
             }
             // the M map with its zero border
@@ -1629,9 +1634,12 @@ constexpr int kStageItems = kSrcRows * 3;
 constexpr int kOrbHItems = 3;          // horizontal items per lane (189 of 192 used)
 constexpr int kOrbCSlots = 4;          // centroid slots per lane (213 of 256 used)
 
-// v_writelane_b32: lane `lane` (wave-uniform) of `old` becomes the uniform `v` (no builtin in this clang)
-// (gfx9 constant-bus rule: with an SGPR value the lane select goes through M0)
-__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v, int lane) {
+// v_writelane_b32 (no clang builtin in this toolchain): lane `lane` (wave-uniform) of `old` becomes the
+// uniform `v`.  gfx9's constant-bus rule puts the lane select in M0, which the asm sets itself.  M0 is a
+// reserved register the compiler does not preserve across inline asm; no other instruction of the kernels
+// that use this reads M0 (no LDS DMA, s_sendmsg, GWS or movrel), which tests/test_build.py checks in the
+// built code object.
+__device__ __forceinline__ uint32_t writelane_m0(uint32_t old, uint32_t v, int lane) {
     asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(v), "s"(lane) : "m0");
     return old;
 }
@@ -1875,8 +1883,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 v2[e] = s >> 16;
             }
             const uint64_t bb = __ballot(v2[0] < v2[1]);
-            mine_lo = writelane(mine_lo, (uint32_t)bb, i);  // lane i keeps this ballot
-            mine_hi = writelane(mine_hi, (uint32_t)(bb >> 32), i);
+            // lane i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
+            // 3-5 % slower, profiles/r02/ab_r2p.log, ab_r2q.log)
+            mine_lo = writelane_m0(mine_lo, (uint32_t)bb, i);
+            mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), i);
         }
         const int o = pre[l] + k0 + j;
         if (lane < 4) *(uint2*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 8 * lane) = uint2{mine_lo, mine_hi};

@@ -1,0 +1,54 @@
+"""Properties of the built gfx950 code objects (CPU only: the library is disassembled, nothing runs)."""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "pyorbslam_amd" / "_lib" / "liborbfe.so"
+OBJDUMP = Path("/opt/rocm/lib/llvm/bin/llvm-objdump")
+
+
+def _disassembly(tmp_path):
+    if not LIB.exists() or not OBJDUMP.exists():
+        pytest.skip("liborbfe.so or llvm-objdump missing")
+    lib = tmp_path / "liborbfe.so"
+    shutil.copy(LIB, lib)  # --offloading writes the bundles next to its input
+    subprocess.run([str(OBJDUMP), "--offloading", str(lib)], cwd=tmp_path, check=True, capture_output=True)
+    objs = sorted(tmp_path.glob("liborbfe.so.*gfx950*"))
+    assert objs, "no gfx950 code object in liborbfe.so"
+    return "\n".join(subprocess.run([str(OBJDUMP), "-d", str(o)], check=True, capture_output=True,
+                                    text=True).stdout for o in objs)
+
+
+def _functions(dis):
+    """{symbol: body} of every kernel in the disassembly."""
+    out, name, body = {}, None, []
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            if name:
+                out[name] = "\n".join(body)
+            name, body = m.group(1), []
+        elif name:
+            body.append(line)
+    if name:
+        out[name] = "\n".join(body)
+    return out
+
+
+def test_m0_only_for_writelane(tmp_path):
+    """k_orb keeps its four ballots with v_writelane_b32 whose lane select the inline asm puts in M0, a
+    register the compiler does not preserve across asm: no other instruction of such a kernel may read
+    or write M0."""
+    funcs = _functions(_disassembly(tmp_path))
+    users = {n: b for n, b in funcs.items() if "v_writelane_b32" in b}
+    assert any("k_orb" in n for n in users), "k_orb no longer uses v_writelane_b32: update this test"
+    for n, b in users.items():
+        for line in b.splitlines():
+            if re.search(r"\bm0\b", line):
+                ins = line.split("//")[0].split()
+                op = next((t for t in ins if re.match(r"^[sv]_|^ds_|^buffer_|^global_", t)), "")
+                assert op in ("s_mov_b32", "v_writelane_b32"), f"{n}: unexpected M0 use: {line.strip()}"
