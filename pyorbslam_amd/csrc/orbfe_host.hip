@@ -665,7 +665,8 @@ hipStream_t own(orbfe_ctx& c) {
 
 // Host image rows -> the pinned staging buffer (one CPU pass), then ONE contiguous host->device copy on s.
 // A hipMemcpy2DAsync straight from pageable memory is staged by the runtime row by row: 6.8 ms per pair
-// of 1241x376 images, against 0.4 ms for the whole pair call this way (r2, tools/dbg/frame_extract_time.py).  The caller synchronises s before h_in is reused.
+// of 1241x376 images, against 0.4 ms for the whole pair call this way (tools/dbg/frame_extract_time.py).
+// The caller synchronises s before h_in is reused.
 void stage_images(orbfe_ctx& c, uint8_t* dst, const uint8_t* const* imgs, int n, int width, int height,
                   int64_t stride, int64_t pitch, hipStream_t s) {
     c.h_in.ensure((size_t)pitch * n);

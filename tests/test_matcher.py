@@ -195,3 +195,101 @@ def test_stacked_projection_equals_per_point_matmul():
             R, t = rng.normal(size=(3, 3)).astype(rdt), rng.normal(size=(3, 1)).astype(rdt)
             X = (rng.normal(size=(2000, 3, 1)) * 30).astype(dt)
             assert np.array_equal(R @ X + t, np.stack([R @ X[k] + t for k in range(len(X))]))
+
+
+def _select_ff_py(off, idx, dist, u, invzc, radius, q_obs, u_right, blocked, mbf, th_high):
+    """ORBMatcher.py:348-372 as written, over the same arrays (Python float arithmetic)."""
+    out = []
+    for q in range(len(off) - 1):
+        best_dist, best = 256, -1
+        for k in range(off[q], off[q + 1]):
+            i2 = int(idx[k])
+            if blocked[i2]:
+                continue
+            if u_right[i2] > 0:
+                ur = float(u[q]) - mbf * float(invzc[q])
+                if abs(ur - float(u_right[i2])) > float(radius[q]):
+                    continue
+            if dist[k] < best_dist:
+                best_dist, best = int(dist[k]), i2
+        if best_dist <= th_high:
+            out.append(best)
+            blocked[best] = q_obs[q]
+        else:
+            out.append(-1)
+    return out
+
+
+def _select_fp_py(off, idx, dist, xr, rs, octv, q_obs, u_right, blocked, nnratio, th_high):
+    """ORBMatcher.py:246-281 as written."""
+    out = []
+    for q in range(len(off) - 1):
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for k in range(off[q], off[q + 1]):
+            i = int(idx[k])
+            if blocked[i]:
+                continue
+            if u_right[i] > 0 and abs(float(xr[q]) - float(u_right[i])) > float(rs[q]):
+                continue
+            d = int(dist[k])
+            if d < bd:
+                bd2, bd, bl2, bl, bi = bd, d, bl, int(octv[i]), i
+            elif d < bd2:
+                bl2, bd2 = int(octv[i]), d
+        if bd <= th_high and not (bl == bl2 and bd > nnratio * bd2):
+            out.append(bi)
+            blocked[bi] = q_obs[q]
+        else:
+            out.append(-1)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_native_selection_matches_python_loop(seed):
+    """orbfe_select_f_f / _f_p (host code) against the reference loops restated in Python, on random
+    candidate sets with stereo gates, pre-blocked slots, ties, empty queries and repeated slots."""
+    from pyorbslam_amd._lib import call, ptr
+    rng = np.random.default_rng(seed)
+    n_frame, nq = 300, 400
+    cnt = rng.integers(0, 12, nq)
+    cnt[rng.random(nq) < 0.1] = 0
+    off = np.zeros(nq + 1, np.int32)
+    np.cumsum(cnt, out=off[1:])
+    idx = rng.integers(0, n_frame, off[-1]).astype(np.int32)
+    dist = rng.integers(0, 140, off[-1]).astype(np.int32)
+    u_right = np.where(rng.random(n_frame) < 0.6, rng.uniform(0, 1200, n_frame), -1.0)
+    blocked0 = (rng.random(n_frame) < 0.1).astype(np.uint8)
+    q_obs = (rng.random(nq) < 0.5).astype(np.uint8)
+    u = rng.uniform(0, 1240, nq)
+    invzc = rng.uniform(0.01, 0.2, nq)
+    radius = rng.uniform(2, 40, nq)
+    mbf = 386.1448
+    got = np.empty(nq, np.int32)
+    blocked = blocked0.copy()
+    call("orbfe_select_f_f", nq, ptr(off), ptr(idx), ptr(dist), ptr(u), ptr(invzc), ptr(radius), ptr(q_obs),
+         ptr(u_right), ptr(blocked), n_frame, mbf, 100, ptr(got))
+    b2 = blocked0.copy()
+    assert got.tolist() == _select_ff_py(off, idx, dist, u, invzc, radius, q_obs, u_right, b2, mbf, 100)
+    assert np.array_equal(blocked, b2)
+    xr = rng.uniform(0, 1240, nq)
+    octv = rng.integers(0, 8, n_frame).astype(np.int32)
+    blocked = blocked0.copy()
+    call("orbfe_select_f_p", nq, ptr(off), ptr(idx), ptr(dist), ptr(xr), ptr(radius), ptr(octv), ptr(q_obs),
+         ptr(u_right), ptr(blocked), n_frame, 0.8, 100, ptr(got))
+    b2 = blocked0.copy()
+    assert got.tolist() == _select_fp_py(off, idx, dist, xr, radius, octv, q_obs, u_right, b2, 0.8, 100)
+    assert np.array_equal(blocked, b2)
+
+
+def test_native_selection_rejects_bad_index():
+    from pyorbslam_amd import _lib
+    off = np.array([0, 2], np.int32)
+    idx = np.array([0, 5], np.int32)  # 5 >= n_frame
+    dist = np.zeros(2, np.int32)
+    z = np.zeros(4, np.float64)
+    flags = np.zeros(4, np.uint8)
+    out = np.empty(1, np.int32)
+    rc = _lib.lib().orbfe_select_f_f(1, _lib.ptr(off), _lib.ptr(idx), _lib.ptr(dist), _lib.ptr(z), _lib.ptr(z),
+                                     _lib.ptr(z), _lib.ptr(flags), _lib.ptr(z), _lib.ptr(flags), 4, 1.0, 100,
+                                     _lib.ptr(out))
+    assert rc < 0 and "out of range" in _lib.lib().orbfe_last_error().decode()
