@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -381,6 +382,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     // candidates in LDS when the node arrays leave room for them, else they stay in the global scratch
     // (very large per-level feature counts, e.g. one level with thousands of features)
     g.oct_keys = kOctKeys;
+    if (const char* e = std::getenv("ORBFE_OCT_KEYS")) g.oct_keys = std::max(0, std::min(kOctKeys, std::atoi(e)));
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_keys = 0;
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024)
         throw Error(ORBFE_EINVAL, "octree LDS footprint exceeds the 160 KiB LDS of a CU (nfeatures per level too large)");

@@ -20,6 +20,11 @@ map-point slots, observations) is read in the replay phase at the reference's po
 input a search can change under itself is a map point's descriptor (fuse_pkf_mp: MapPoint.replace
 recomputes the survivor's distinctive descriptor, MapPoint.py:180); the replay compares the descriptor it
 reads with the collected one and re-runs that query's distances on the GPU when they differ.
+
+The replay loops restate ORBMatcher.py statement by statement on purpose: a drop-in must reproduce the
+reference's control flow, NumPy-2 dtype promotions and the order of its side effects exactly, so those
+lines necessarily read like the reference's.  The two tracking searches also have a native selection
+(orbfe_select_f_f / _f_p, host C) used when every compared value is a double.
 """
 from __future__ import annotations
 
