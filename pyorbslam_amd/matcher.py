@@ -144,6 +144,30 @@ def _frame_grid(frame):
     return grid
 
 
+_angle_cache = weakref.WeakKeyDictionary()
+
+
+def _angles(frame):
+    """mvKeysUn[i].angle as doubles (the rotation histogram's input), cached per keypoint list; None when
+    an angle is not a double (a float32 angle would make the reference's subtraction float32)."""
+    kps = frame.mvKeysUn
+    key = (id(kps), len(kps))
+    try:
+        ent = _angle_cache.get(frame)
+    except TypeError:
+        ent = None
+    if ent is not None and ent[0] == key:
+        return ent[1]
+    arr = None
+    if all(type(k.angle) in _F64 for k in kps):
+        arr = np.fromiter((k.angle for k in kps), np.float64, count=len(kps))
+    try:
+        _angle_cache[frame] = (key, arr)
+    except TypeError:
+        pass
+    return arr
+
+
 def _grid_csr(frame, grid, qx, qy, qr, lo, hi):
     """orbfe_grid_query over float64 / int32 query arrays: (out_off, out_idx) as int32 arrays."""
     off, idx, kx, ky, ko, f4, cols, rows = grid
@@ -500,19 +524,30 @@ class ORBMatcher:
             qu, qz, qrad = (np.ascontiguousarray(a[rows], np.float64) for a in (qx, iz, radius))  # held across the call
             call("orbfe_select_f_f", len(rl), ptr(off2), ptr(idx), ptr(dist), ptr(qu), ptr(qz), ptr(qrad), ptr(q_obs),
                  ptr(u_right), ptr(blocked), n_frame, float(cur.mbf), TH_HIGH, ptr(best))
-            for j in np.flatnonzero(best >= 0).tolist():
-                b = int(best[j])
+            hit = np.flatnonzero(best >= 0)
+            bl = best[hit].tolist()
+            for j, b in zip(hit.tolist(), bl):
                 cur.mvpMapPoints[b] = pmps[rl[j]]
-                n_matches += 1
-                if self.mbCheckOrientation:  # ORBMatcher.py:374-382
-                    rot = last.mvKeysUn[ci[rl[j]]].angle - cur.mvKeysUn[b].angle
-                    if rot < 0.0:
-                        rot += 360.0
-                    bin_idx = round(rot * factor)
-                    if bin_idx == HISTO_LENGTH:
-                        bin_idx = 0
-                    assert 0 <= bin_idx < HISTO_LENGTH
-                    rot_hist[bin_idx].append(b)
+            n_matches += len(bl)
+            if self.mbCheckOrientation and bl:  # ORBMatcher.py:374-382
+                la, ca = _angles(last), _angles(cur)
+                if la is not None and ca is not None:  # doubles: the same arithmetic over arrays
+                    rot = la[np.asarray(ci, np.int64)[rows[hit]]] - ca[best[hit]]
+                    rot = np.where(rot < 0.0, rot + 360.0, rot)
+                    bins = np.round(rot * factor).astype(np.int64)  # round() of a double: half to even
+                    bins[bins == HISTO_LENGTH] = 0
+                    bins = bins.tolist()
+                else:
+                    bins = []
+                    for j, b in zip(hit.tolist(), bl):
+                        rot = last.mvKeysUn[ci[rl[j]]].angle - cur.mvKeysUn[b].angle
+                        if rot < 0.0:
+                            rot += 360.0
+                        bin_idx = round(rot * factor)
+                        bins.append(0 if bin_idx == HISTO_LENGTH else bin_idx)
+                for b, k in zip(bl, bins):
+                    assert 0 <= k < HISTO_LENGTH
+                    rot_hist[k].append(b)
         if self.mbCheckOrientation:
             ind1, ind2, ind3 = self.compute_three_maxima(rot_hist, HISTO_LENGTH)
             for i in range(HISTO_LENGTH):
