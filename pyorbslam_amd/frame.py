@@ -217,12 +217,45 @@ def undistort_keypoints(self):
     return self.mvKeysUn
 
 
+def assign_features_to_grid(self) -> None:
+    """Frame.assign_features_to_grid + pos_in_grid (Frame.py:143-159) with the per-keypoint Python loop
+    replaced by array operations: the same positions (np.round of the same float64 expression), the same
+    column-major mGrid of Python lists holding keypoint indices in increasing order.  The grid is also
+    kept as CSR arrays (_orbfe_grid) for the matcher's batched window queries.  Frames whose keypoint
+    coordinates are not Python floats, or with no keypoints (where the reference's pos_in_grid raises),
+    run the reference method."""
+    kps, n = self.mvKeys, self.N
+    ref = getattr(type(self), "_orbfe_ref_assign", None)
+    if n == 0 or len(kps) != n or type(kps[0].pt[0]) is not float:
+        if ref is None:
+            raise RuntimeError("install() did not record the reference assign_features_to_grid")
+        return ref(self)
+    pts = np.fromiter((c for kp in kps for c in kp.pt), np.float64, count=2 * n).reshape(n, 2)
+    px = np.round((pts[:, 0] - self.mnMinX) * self.mfGridElementWidthInv).astype(int)
+    py = np.round((pts[:, 1] - self.mnMinY) * self.mfGridElementHeightInv).astype(int)
+    cols, rows = self.FRAME_GRID_COLS, self.FRAME_GRID_ROWS
+    valid = (px >= 0) & (px < cols) & (py >= 0) & (py < rows)
+    keep = np.flatnonzero(valid)
+    cell = px[keep] * rows + py[keep]
+    order = np.argsort(cell, kind="stable")  # by cell, then by keypoint index (the reference's append order)
+    flat = keep[order].astype(np.int32)
+    off = np.zeros(cols * rows + 1, np.int32)
+    np.cumsum(np.bincount(cell, minlength=cols * rows), out=off[1:])
+    fl, o = flat.tolist(), off.tolist()
+    self.mGrid = [[fl[o[ix * rows + iy]:o[ix * rows + iy + 1]] for iy in range(rows)] for ix in range(cols)]
+    self._orbfe_grid = (id(self.mGrid), off, flat)
+
+
 def install(frame_cls, copy: bool = True, pair: bool = True) -> None:
-    """Replace Frame.compute_stereo_matches (Frame.py:161), Frame.undistort_keypoints (Frame.py:293), unless
+    """Replace Frame.compute_stereo_matches (Frame.py:161), Frame.undistort_keypoints (Frame.py:293),
+    Frame.assign_features_to_grid (Frame.py:152), unless
     pair=False Frame.ExtractORB (Frame.py:114: both images in one enqueue) and unless copy=False Frame.copy
     (Frame.py:75) of the reference class in place."""
     frame_cls.compute_stereo_matches = compute_stereo_matches
     frame_cls.undistort_keypoints = undistort_keypoints
+    if frame_cls.__dict__.get("assign_features_to_grid") is not assign_features_to_grid:
+        frame_cls._orbfe_ref_assign = getattr(frame_cls, "assign_features_to_grid", None)
+    frame_cls.assign_features_to_grid = assign_features_to_grid
     if pair:
         frame_cls.ExtractORB = extract_orb
     if copy:

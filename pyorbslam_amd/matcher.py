@@ -130,11 +130,15 @@ def _frame_grid(frame):
     if not all(type(v) in _F64 for v in f4):
         return None
     cols, rows = frame.FRAME_GRID_COLS, frame.FRAME_GRID_ROWS
-    sizes = np.fromiter((len(frame.mGrid[ix][iy]) for ix in range(cols) for iy in range(rows)), np.int32,
-                        count=cols * rows)
-    off = np.zeros(cols * rows + 1, np.int32)
-    np.cumsum(sizes, out=off[1:])
-    idx = np.fromiter((g for col in frame.mGrid for cell in col for g in cell), np.int32, count=int(off[-1]))
+    csr = getattr(frame, "_orbfe_grid", None)  # left by frame.assign_features_to_grid for this mGrid
+    if csr is not None and csr[0] == id(frame.mGrid) and len(csr[1]) == cols * rows + 1:
+        off, idx = csr[1], csr[2]
+    else:
+        sizes = np.fromiter((len(frame.mGrid[ix][iy]) for ix in range(cols) for iy in range(rows)), np.int32,
+                            count=cols * rows)
+        off = np.zeros(cols * rows + 1, np.int32)
+        np.cumsum(sizes, out=off[1:])
+        idx = np.fromiter((g for col in frame.mGrid for cell in col for g in cell), np.int32, count=int(off[-1]))
     kps = frame.mvKeysUn
     kx = np.fromiter((k.pt[0] for k in kps), np.float64, count=len(kps))
     ky = np.fromiter((k.pt[1] for k in kps), np.float64, count=len(kps))
