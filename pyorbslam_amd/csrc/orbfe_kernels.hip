@@ -2076,10 +2076,45 @@ __device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int 
         if (j < n) dst[j] = v[j];
 }
 
+// sheared_row's run of n <= 24 bytes, returned as 6 dwords (byte j of the run = byte j % 4 of w[j / 4])
+__device__ __forceinline__ void sheared_words(const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
+                                              uint32_t (&wd)[6]) {
+    const int pw = w + 2 * kEdge;
+    const int f = kEdge * pw + kEdge + r * w + c0;
+    int pr = f / pw, pc = f - pr * pw;
+    if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
+        uint32_t bias;  // lvl differs between the 16-lane groups of a wave (one keypoint and octave each)
+        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc_lane(lvl, (uint32_t)(stride * h), &bias);
+        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge)) + bias;
+        const uint32_t sh = off & 3u, al = off - sh;
+        uint32_t d[7];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * k, 0, 0);
+        d[6] = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) wd[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wd[k] = 0;
+#pragma unroll
+    for (int j = 0; j < 21; ++j) {
+        if (j < n) wd[j >> 2] |= (uint32_t)lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)]
+                                 << (8 * (j & 3));
+        if (++pc == pw) {
+            pc = 0;
+            ++pr;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     __shared__ int sad[16][11];
-    __shared__ uint8_t sL[16][121];
-    __shared__ uint8_t sR[16][231];
+    // the 11 x 11 left and 11 x 21 right windows as u16 pixel + 512: left columns (2k, 2k + 1) per dword,
+    // right columns (2k, 2k + 1) and (2k + 1, 2k + 2) per dword (both alignments of a shift's window)
+    __shared__ uint32_t sP[16][11][6];
+    __shared__ uint32_t sE[16][11][11];
+    __shared__ uint32_t sO[16][11][10];
     // per-octave geometry (scale, inverse scale, w, h, pitch, ws_off) in LDS: indexed by a keypoint's octave
     // the kernel argument would be read with vector memory loads, two dependent round trips in the refine
     __shared__ float s_sc[kMaxLevels], s_isc[kMaxLevels];
@@ -2180,9 +2215,31 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
                  scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
-        if (do_sad && sl < 11) {
-            sheared_row(lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, &sL[kq][sl * 11]);
-            sheared_row(lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, &sR[kq][sl * 21]);
+        if (do_sad && sl < 11) {  // lane sl stages window row sl
+            uint32_t wl[6], wr[6];
+            sheared_words(lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, wl);
+            sheared_words(lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, wr);
+            constexpr uint32_t k512 = 0x02000200u;
+            // bytes (b, b + 1) of a dword pair as two u16 (0x0c selects a zero byte)
+            auto lo2 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c010c00u); };
+            auto hi2 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c02u); };
+            auto mid2 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c01u); };
+            auto cross2 = [](uint32_t x, uint32_t nx) { return __builtin_amdgcn_perm(nx, x, 0x0c040c03u); };
+            auto add = [](uint32_t a, uint32_t b) {
+                return __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, a) + __builtin_bit_cast(us2, b));
+            };
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                sP[kq][sl][2 * k] = add(lo2(wl[k]), k512);
+                sP[kq][sl][2 * k + 1] = add(hi2(wl[k]), k512);
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                if (2 * k < 11) sE[kq][sl][2 * k] = add(lo2(wr[k]), k512);
+                if (2 * k + 1 < 11) sE[kq][sl][2 * k + 1] = add(hi2(wr[k]), k512);
+                if (2 * k < 10) sO[kq][sl][2 * k] = add(mid2(wr[k]), k512);
+                if (2 * k + 1 < 10) sO[kq][sl][2 * k + 1] = add(cross2(wr[k], k + 1 < 6 ? wr[k + 1] : 0u), k512);
+            }
         }
     }
     // sL / sR / sad are per 16-lane group, i.e. per wavefront: a wavefront barrier orders them (the
@@ -2190,20 +2247,30 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (do_sad) {
-        const int lc = sL[kq][60];  // IL[5][5]
-        // 11 shifts x 11 rows = 121 row sums of 11 |(IL - IL[5,5]) - (IR - IR[5,5])| terms
-        for (int it = sl; it < 121; it += 16) {
-            const int s = it / 11, r = it - s * 11;
-            const int rc = sR[kq][5 * 21 + s + 5];
-            int acc = 0;
+    if (do_sad && sl < 11) {
+        // lane s: SAD of shift s, sum over the 11 rows of |(IL - IL[5,5]) - (IR - IR[5,5 + s])| =
+        // |(IL + 512 + d) - (IR + 512)| with d = IR[5,5 + s] - IL[5,5] (the left term stays in [257, 1022]:
+        // exact in u16), two columns per v_sad_u16; the 12th column of the last pair is masked to zero
+        const int s = sl;
+        const int lc = (int)((sP[kq][5][2] >> 16) & 0xFFFFu);  // IL[5][5] + 512
+        const uint32_t rw = sE[kq][5][(s + 5) >> 1];  // columns (s + 4, s + 5) or (s + 5, s + 6)
+        const int rc = (int)((s & 1) ? (rw & 0xFFFFu) : (rw >> 16));  // IR[5][5 + s] + 512
+        const uint32_t d = (uint32_t)(rc - lc) & 0xFFFFu;
+        const uint32_t dd = d | (d << 16);
+        const int b0 = s >> 1;
+        uint32_t acc = 0;
 #pragma unroll
-            for (int c = 0; c < 11; ++c) {
-                const int dd = (sL[kq][r * 11 + c] - lc) - (sR[kq][r * 21 + s + c] - rc);
-                acc += dd < 0 ? -dd : dd;
+        for (int r = 0; r < 11; ++r) {
+            const uint32_t* bp = (s & 1) ? &sO[kq][r][b0] : &sE[kq][r][b0];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const uint32_t a = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, sP[kq][r][k]) +
+                                                                    __builtin_bit_cast(us2, dd));
+                const uint32_t b = bp[k];
+                acc = k < 5 ? __builtin_amdgcn_sad_u16(a, b, acc) : __builtin_amdgcn_sad_u16(a & 0xFFFFu, b & 0xFFFFu, acc);
             }
-            atomicAdd(&sad[kq][s], acc);
         }
+        sad[kq][s] = (int)acc;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
