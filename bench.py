@@ -263,7 +263,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--pairs", type=int, default=256, help="stereo pairs per step per GPU")
+    ap.add_argument("--pairs", type=int, default=512, help="stereo pairs per step per GPU (256: -1.7 %%, tools/dbg/pairs_sweep.sh)")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--nfeatures", type=int, default=2000)

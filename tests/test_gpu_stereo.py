@@ -293,19 +293,20 @@ def test_undistort_keypoints_drop_in():
 
 
 def test_default_bench_configuration_sampled():
-    """The exact default bench step (256 KITTI pairs as 4 handles x 64 pairs on 4 streams, lanes 1) and the
+    """The exact default bench step (512 KITTI pairs as 4 handles x 128 pairs on 4 streams, lanes 1) and the
     bench's own parity check: every handle's overflow word, its first and last pair bit for bit against the
     oracle extractor and the stereo restatement."""
     torch = pytest.importorskip("torch")
     import bench
     from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
-    host = synth.make_batch(256, seed0=0)
+    P, S = 512, 4
+    host = synth.make_batch(P, seed0=0)
     images = torch.from_numpy(host).cuda()
-    fes = [StereoFrontEnd(max_pairs=64, lanes=1, blur_fork=False) for _ in range(4)]
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(3)]
+    fes = [StereoFrontEnd(max_pairs=P // S, lanes=1, blur_fork=False) for _ in range(S)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     for _ in range(2):  # the bench repeats the step on the same buffers
         for i, (f, st) in enumerate(zip(fes, streams)):
-            f.enqueue(images[128 * i:128 * (i + 1)], 64, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
+            f.enqueue(images[2 * (P // S) * i:2 * (P // S) * (i + 1)], P // S, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
     torch.cuda.synchronize()
-    checked, ovf, bad = bench.parity_check(fes, host, 64, 1241, 376, 2000)
+    checked, ovf, bad = bench.parity_check(fes, host, P // S, 1241, 376, 2000)
     assert ovf == 0 and not bad and checked == 8, bad
