@@ -270,9 +270,6 @@ def main():
     ap.add_argument("--streams", type=int, default=4,
                     help="independent front-end handles per GPU, each on its own stream with P/streams pairs")
     ap.add_argument("--lanes", type=int, default=1, help="internal concurrent chunks per handle (orbfe_set_lanes)")
-    ap.add_argument("--blur-fork", type=int, default=0,
-                    help="k_blur on a side stream per handle (orbfe_set_blur_fork); off by default: the 4 handles "
-                         "already fill the 4 hardware queues (GPU_MAX_HW_QUEUES), side streams would share them")
     ap.add_argument("--cpu-sample", type=int, default=40,
                     help="pairs timed on 1 thread for cpu_baseline (0 = skip); the all-cores figure adds 4 per process")
     ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = this "
@@ -331,8 +328,7 @@ def main():
     if not args.roofline_only:
         # S sub-batches of P/S pairs, each with its own handle (buffers) and stream, so that the latency-bound
         # stages of one overlap the issue-bound stages of another; every pair is still processed exactly once
-        fes = [StereoFrontEnd(args.width, args.height, max_pairs=per, nfeatures=args.nfeatures, lanes=args.lanes,
-                              blur_fork=bool(args.blur_fork)) for _ in range(S)]
+        fes = [StereoFrontEnd(args.width, args.height, max_pairs=per, nfeatures=args.nfeatures, lanes=args.lanes) for _ in range(S)]
         streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
         subs = [images[2 * per * i: 2 * per * (i + 1)] for i in range(S)]
 
@@ -387,7 +383,7 @@ def main():
     if args.roofline_steps > 0 and rank == 0:
         del fes
         torch.cuda.synchronize(dev)
-        solo = StereoFrontEnd(args.width, args.height, max_pairs=P, nfeatures=args.nfeatures, lanes=1, blur_fork=False)
+        solo = StereoFrontEnd(args.width, args.height, max_pairs=P, nfeatures=args.nfeatures, lanes=1)
         st0 = torch.cuda.current_stream(dev)
         for _ in range(2):
             solo.enqueue(images, P, KITTI_BF, KITTI_FX, stream_ptr=st0.cuda_stream)
@@ -422,7 +418,7 @@ def main():
             "config": {"workload": workload, "pairs_per_step_per_gpu": P, "width": args.width, "height": args.height,
                        "nfeatures": args.nfeatures, "nlevels": 8, "scaleFactor": 1.2, "iniThFAST": 20, "minThFAST": 7,
                        "parallelism": f"pairs sharded {world}-way (independent replicas, no data-path collective)",
-                       "handles_per_gpu": S, "lanes_per_handle": args.lanes, "blur_side_stream": bool(args.blur_fork)},
+                       "handles_per_gpu": S, "lanes_per_handle": args.lanes},
         })
         if parity is not None:
             out.update(parity)

@@ -165,9 +165,9 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
  * their layout do not depend on it. */
 int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
 
-/* orbfe_set_blur_fork: run k_blur on an internal side stream, concurrently with FAST and the octree
- * (on = 1, default), or in order on the launch stream (on = 0: one stream per handle, for callers that
- * already run several handles on their own streams).  Results do not depend on it. */
+/* orbfe_set_blur_fork: accepted and ignored (kept for ABI stability).  Round 1 ran a full-pyramid k_blur
+ * that could fork onto a side stream; the blur is now fused into the descriptor kernel (k_orb), which
+ * blurs only each keypoint's neighbourhood, so there is nothing to fork. */
 int orbfe_set_blur_fork(orbfe_handle h, int32_t on);
 
 /* Device result layout of the last batch (pointers into handle-owned device memory):
@@ -282,8 +282,8 @@ int orbfe_png_read_batch(const char* const* paths, int32_t n, int32_t width, int
 
 /* ---- live stage timing --------------------------------------------------------------------------
  * While profiling is on, every batch enqueued on the handle records HIP events around its stages:
- * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 blur (k_blur, timed on the side
- * stream it runs on, concurrently with detect/octree), 4 describe (IC angle + BRIEF), 5 stereo.
+ * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 blur (empty: fused into describe),
+ * 4 describe (k_orb: IC angle + per-keypoint 7x7 blur + steered BRIEF), 5 stereo.
  * orbfe_profile_read synchronises and returns the summed milliseconds per stage (ms_per_stage holds
  * ORBFE_NSTAGES floats) over the recorded batches. */
 #define ORBFE_NSTAGES 6

@@ -16,14 +16,12 @@ constexpr int kBorder = kEdge - 3; // minBorderX/Y (ORBextractor.cpp:772-773)
 constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
 constexpr int kPatchR = 21;        // descriptor patch radius: 18 (max rotated pattern offset) + 3 (blur)
 constexpr int kPatchD = 2 * kPatchR + 1;  // 43
-constexpr int kBlurR = 18;
-constexpr int kBlurD = 2 * kBlurR + 1;    // 37
 constexpr int kMaxCellRoi = 64;    // max cell ROI side (wCell+6, hCell+6); checked on the host
 
 // One pyramid level of one image geometry.
 struct LevelGeo {
     int w, h;            // level size: cvRound(W * invScale), cvRound(H * invScale) (:1110-1111)
-    int pitch;           // row pitch of the level in the pyramid / blur workspaces (w rounded up to 16)
+    int pitch;           // row pitch of the level in the pyramid workspace (w rounded up to 16)
     int64_t ws_off;      // byte offset of the level inside an image's pyramid workspace (levels >= 1)
     float scale, inv_scale;
     int n_feat;          // mnFeaturesPerLevel[l]
@@ -41,8 +39,6 @@ struct LevelGeo {
     int xtab_off, ytab_off;
     int xmax;            // first column whose sx+1 >= src width
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
-    int64_t blur_off;    // byte offset of the blurred level inside an image's blur workspace
-    int blur_tile0;      // first k_blur tile of this level (64 x 32 tiles)
     // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;
     // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
     int rs_ngrp, rs_nsrc, rs_sp;
@@ -58,8 +54,6 @@ struct CellGeo {
 };
 
 // Resize column entry.
-// k_blur output tile (the host counts tiles per level with the same numbers)
-constexpr int kBlurTX = 64, kBlurTY = 58;
 constexpr int kRsRows = 16;  // k_resize output rows per workgroup (band)
 // k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
 constexpr int kOctKeys = 7424;
@@ -82,8 +76,6 @@ struct Geo {
     int kp_cap;          // per-image capacity of the final keypoint list (sum of level kp_cap)
     int lvl_kp_cap;      // per-image size of the level-keypoint array (same as kp_cap)
     int64_t ws_bytes;    // per-image pyramid workspace bytes (levels >= 1)
-    int64_t blur_bytes;  // per-image blurred-pyramid bytes (all levels)
-    int blur_tiles;      // k_blur tiles per image
     int64_t shear_bytes; // per-image k_shear output (sum of w x h over levels)
     int64_t slot_total;  // per-image cell slot count
     int64_t key_total;   // per-image dense candidate scratch count

@@ -61,12 +61,10 @@ struct orbfe_ctx {
 
     DevBuf<CellGeo> d_cells;
     DevBuf<ResizeX> d_xt;
-    DevBuf<uint32_t> d_mw;  // k_describe: [4 row shifts][31 x 9 window dwords] (disc byte mask, m10 weights)
     DevBuf<uint32_t> d_orb; // k_orb: horizontal items of the sample disc + centroid slots (orb_tables)
     DevBuf<ResizeY> d_yt;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
-    DevBuf<uint8_t> d_blur;
     DevBuf<int> d_cell_count;
     DevBuf<uint32_t> d_slots;
     DevBuf<uint32_t> d_kd;
@@ -97,13 +95,8 @@ struct orbfe_ctx {
     bool prof_on = false;
 
     hipStream_t own_stream = nullptr;
-    // k_blur runs on a side stream concurrently with k_detect / k_octree (fork after the pyramid, join
-    // before k_describe); events only, so the batch stays capturable into a HIP graph
-    hipStream_t side_stream[kLanes + 1] = {};
-    hipEvent_t ev_fork[kLanes + 1] = {}, ev_join[kLanes + 1] = {};
     // orbfe_frontend_batch_device: up to kLanes concurrent chunks of the batch on internal streams
     int lanes = kLanes;  // orbfe_set_lanes
-    bool blur_fork = true;  // orbfe_set_blur_fork
     hipStream_t lane_stream[kLanes] = {};
     hipEvent_t lane_done[kLanes] = {};
     hipEvent_t lane_fork = nullptr;
@@ -129,9 +122,6 @@ struct orbfe_ctx {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
         for (int k = 0; k <= kLanes; ++k) {
-            if (side_stream[k]) (void)hipStreamDestroy(side_stream[k]);
-            if (ev_fork[k]) (void)hipEventDestroy(ev_fork[k]);
-            if (ev_join[k]) (void)hipEventDestroy(ev_join[k]);
         }
         for (int k = 0; k < kLanes; ++k) {
             if (lane_stream[k]) (void)hipStreamDestroy(lane_stream[k]);
@@ -254,8 +244,8 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.xt.clear();
     c.yt.clear();
     c.maxcell = 0;
-    int64_t ws = 0, bws = 0, shear = 0;
-    int kp_off = 0, key_off = 0, btile = 0;
+    int64_t ws = 0, shear = 0;
+    int kp_off = 0, key_off = 0;
     int64_t slot_off = 0;
     for (int l = 0; l < L; ++l) {
         LevelGeo& Lg = g.lv[l];
@@ -277,10 +267,6 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         }
         Lg.shear_off = shear;
         shear += ((int64_t)Lg.w * Lg.h + 3) & ~(int64_t)3;
-        Lg.blur_off = bws;
-        bws += ((int64_t)Lg.pitch * Lg.h + 255) & ~(int64_t)255;
-        Lg.blur_tile0 = btile;
-        btile += ((Lg.w + kBlurTX - 1) / kBlurTX) * ((Lg.h + kBlurTY - 1) / kBlurTY);
         Lg.n_feat = c.n_per_level[l];
         Lg.size = (float)(int)(31 * c.sf[l]);
         // cell grid (ORBextractor.cpp:772-806)
@@ -373,8 +359,6 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     if ((int64_t)g.rs_ngrp * 36 + 128 + (int64_t)g.rs_nsrc * g.rs_sp + 16 > 150 * 1024)
         throw Error(ORBFE_EINVAL, "image too wide for the k_resize band staging (LDS)");
     g.ws_bytes = std::max<int64_t>(ws, 256);
-    g.blur_bytes = bws;
-    g.blur_tiles = btile;
     g.shear_bytes = shear;
     g.slot_total = std::max<int64_t>(slot_off, 1);
     g.key_total = std::max(key_off, 1);
@@ -444,22 +428,6 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
         HIPCK(hipMemcpy(c.d_cells.p, c.cells.data(), c.cells.size() * sizeof(CellGeo), hipMemcpyHostToDevice));
-        {   // centroid masks/weights of k_describe, a function of umax only
-            std::vector<uint32_t> mw(4 * 31 * 9 * 2);
-            for (int sh = 0; sh < 4; ++sh)
-                for (int slot = 0; slot < 31 * 9; ++slot) {
-                    const int r = slot / 9, d = slot % 9, v = r - kHalfPatch, um = c.umax[v < 0 ? -v : v];
-                    const int u0 = 4 * d - sh - kHalfPatch;
-                    const int blo = std::min(std::max(-um - u0, 0), 4), bhi = std::min(std::max(um - u0 + 1, 0), 4);
-                    const int n = bhi - blo;
-                    const uint32_t mask = n > 0 ? (0xFFFFFFFFu >> (32 - 8 * n)) << (8 * blo) : 0u;
-                    const uint32_t w = (uint32_t)(u0 + 18) * 0x01010101u + 0x03020100u;  // byte weights u0 + 18 + b
-                    mw[2 * (sh * 279 + slot)] = mask;
-                    mw[2 * (sh * 279 + slot) + 1] = w;
-                }
-            c.d_mw.ensure(mw.size());
-            HIPCK(hipMemcpy(c.d_mw.p, mw.data(), mw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        }
         {
             const std::vector<uint32_t> ot = orb_tables(c.umax);
             c.d_orb.ensure(ot.size());
@@ -502,18 +470,18 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
 }
 
 // record event `k` of the current profiled batch.  Launch stream: 0 start, 1 after resize, 2 after
-// detect, 3 after octree, 4 blur joined (describe starts), 5 after describe, 6 after stereo; the blur
-// stream: 7 before k_blur, 8 after it.  Stage k spans events kProfFrom[k] -> kProfTo[k].
+// detect, 3 after octree, 4 describe (k_orb) starts, 5 after describe, 6 after stereo; 7 / 8 bracket the
+// blur stage, which is empty since the blur was fused into k_orb (kept so the stage list of the ABI stays
+// stable).  Stage k spans events kProfFrom[k] -> kProfTo[k].
 void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
     if (!c.prof_on || c.prof_n >= c.prof_max) return;
     HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * kProfEvents + k], s));
 }
 
 // Images [i0, i0 + n) of the batch: every per-image buffer is passed at the chunk's offset, the
-// kernels index images from there.  prof: record stage boundaries on s.  fork_blur: run k_blur on the
-// side stream concurrently with k_detect / k_octree.
+// kernels index images from there.  prof: record stage boundaries on s.
 void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int n, hipStream_t s, bool prof,
-                   bool fork_blur, int lane = -1) {
+                   int lane = -1) {
     const Geo& g = c.geo;
     const uint8_t* in = d_in + (int64_t)i0 * pitch;
     uint8_t* ws = c.d_ws.p + (int64_t)i0 * g.ws_bytes;
@@ -529,7 +497,6 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     if (prof) prof_mark(c, s, 0);
     for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
     if (prof) prof_mark(c, s, 1);
-    (void)fork_blur;
     (void)lane;
     if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
     if (prof) prof_mark(c, s, 2);
@@ -554,7 +521,7 @@ void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hi
     if (n <= 0) return;
     check_extract(c, pitch, n);
     HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
-    extract_range(c, d_in, pitch, 0, n, s, true, c.blur_fork);
+    extract_range(c, d_in, pitch, 0, n, s, true);
     c.last_in = d_in;
     c.last_pitch = pitch;
     c.last_images = n;
@@ -627,7 +594,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
     const int K = std::max(1, std::min(c.lanes, n_pairs));
     if (K == 1) {
-        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true, c.blur_fork);
+        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true);
         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
         prof_mark(c, s, 6);
     } else {
@@ -643,7 +610,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             const int p0 = (int)((int64_t)n_pairs * k / K), p1 = (int)((int64_t)n_pairs * (k + 1) / K);
             hipStream_t ls = c.lane_stream[k];
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
-            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, c.blur_fork, k);
+            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k);
             stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
             if (k == 0) prof_mark(c, ls, 6);
             HIPCK(hipEventRecord(c.lane_done[k], ls));
@@ -1014,7 +981,7 @@ int orbfe_set_lanes(orbfe_handle h, int32_t lanes) {
 int orbfe_set_blur_fork(orbfe_handle h, int32_t on) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
-        h->blur_fork = on != 0;
+        (void)on;  // accepted for ABI stability: the blur is fused into k_orb, there is no blur stage to fork
     });
 }
 
@@ -1380,23 +1347,10 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
                     break;
                 case 3:
-                    // variant 0: k_orb (production, blur fused), 8: k_orb with 8-wave workgroups, 12 / 9 / 10: 2 / 4 / 16 keypoints
-                    // per wave; the unfused
-                    // pair for comparison: 1 k_blur, 2 k_describe (after a variant-1 run), 3 both, 4 k_describe
-                    // with 4-wave workgroups, 5 k_blur without its stores (probe)
-                    if (variant == 0 || variant == 8 || variant == 9 || variant == 10 || variant == 12) {
-                        HIPCK(launch_orb(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
-                                         h->d_kps.p, h->d_desc.p, h->d_count.p, n, h->d_orb.p, s,
-                                         variant == 12 ? 2 : variant));
-                        break;
-                    }
-                    h->d_blur.ensure((size_t)n * g.blur_bytes);
-                    if (variant == 1 || variant == 3 || variant == 5)
-                        HIPCK(launch_blur(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, n, s, variant == 5));
-                    if (variant == 2 || variant == 3 || variant == 4)
-                        HIPCK(launch_describe(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_blur.p, h->d_lvl_kp.p,
-                                              h->d_lvl_count.p, h->d_kps.p, h->d_desc.p, h->d_count.p, h->d_mw.p,
-                                              n, s, variant == 4 ? 4 : 0));
+                    // variant 0: k_orb (production), 8: 8-wave workgroups, 12 / 9 / 10: 2 / 4 / 16 keypoints per
+                    // wave (the round-1 unfused k_blur + k_describe pair is in the git history, round 1)
+                    HIPCK(launch_orb(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_lvl_kp.p, h->d_lvl_count.p,
+                                     h->d_kps.p, h->d_desc.p, h->d_count.p, n, h->d_orb.p, s, variant == 12 ? 2 : variant));
                     break;
                 case 4:
                     if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");

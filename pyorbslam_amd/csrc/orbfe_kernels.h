@@ -69,11 +69,6 @@ size_t detect_lds_bytes(const Geo& g);
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
                          uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
                          hipStream_t s, int variant = 0, long long* prof = nullptr);
-hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* blur, int n_images,
-                       hipStream_t s, int probe = 0);
-hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
-                           const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
-                           int* out_count, const uint32_t* mw, int n_images, hipStream_t s, int variant = 0);
 // fused IC angle + 7x7 blur of each keypoint's neighbourhood + steered BRIEF (replaces k_blur + k_describe)
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,

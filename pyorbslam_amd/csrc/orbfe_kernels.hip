@@ -4,8 +4,8 @@
 //   k_detect     per-cell FAST-9/16 + 3x3 NMS + iniTh/minTh fallback + ordered compaction
 //                (ComputeKeyPointsOctTree cell loop, ORBextractor.cpp:768-828)
 //   k_octree     DistributeOctTree (ORBextractor.cpp:539-762), one workgroup per (level, image)
-//   k_describe   IC_Angle + GaussianBlur 7x7 + steered BRIEF, one wavefront per keypoint
-//                (ORBextractor.cpp:77-147, 1074-1103)
+//   k_orb        IC_Angle + GaussianBlur 7x7 (per keypoint neighbourhood) + steered BRIEF, one wavefront
+//                per keypoint (ORBextractor.cpp:77-147, 1074-1103)
 //   k_stereo     Frame.compute_stereo_matches (Frame.py:161-279), one wavefront per left keypoint
 //   k_hamming_*  ORBMatcher.descriptor_distance batched (ORBMatcher.py:12-14)
 //
@@ -1186,427 +1186,9 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 }
 
 
-// ------------------------------------------------------------------------------- k_blur
-// cv::GaussianBlur(level clone, 7x7, sigma 2, BORDER_REFLECT_101) for every level of every image, the
-// bit-exact 8U fixed-point path: out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
-// One 256-thread workgroup per kBlurTX x kBlurTY output tile.
-//  * staging: the 64-row x 72-column input window (rows Y0-3 .., columns X0-4 ..) as 18 re-aligned dwords
-//    per row, 3 per dwordx4 load, all loads issued before the first wait; rows go through reflect-101, and the <= 3 columns
-//    left of 0 / right of w-1 of edge tiles are patched in LDS from their reflect-101 sources.
-//  * horizontal: 4 adjacent pixels of 2 rows per thread step from 3 aligned LDS dwords per row, 10
-//    v_dot4_u32_u8 with shifted byte weights per 4 outputs (no v_alignbyte); stored row-pair interleaved,
-//    so a dword holds (H[2m][x], H[2m+1][x]).
-//  * vertical: tile rows 4q .. 4q+3 from the 5 interleaved dwords P(2q) .. P(2q+4) (1.25 LDS reads per
-//    output row), 4 x v_dot2_u32_u16 per row with the +2^15 rounding as the accumulator seed; 4 aligned
-//    dword stores.
-constexpr int kBlurWR = kBlurTY + 6;        // staged window rows
-static_assert((kBlurWR / 2) * (kBlurTX / 4) % 256 == 0, "horizontal items: a whole number per thread");
-constexpr int kBlurWD = (kBlurTX + 8) / 4;  // staged dwords per row (18)
-constexpr int kBlurSD = 20;                 // LDS pitch of a staged row, dwords
-
 __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clamped for far-out rows
     p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
     return min(max(p, 0), n - 1);
-}
-
-__global__ __launch_bounds__(256) void k_blur(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
-                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ blur, int probe) {
-    __shared__ __attribute__((aligned(16))) uint32_t src[kBlurWR * kBlurSD];
-    __shared__ __attribute__((aligned(16))) uint32_t hor[(kBlurWR / 2) * kBlurTX];
-    int bx, img;
-    xcd_block(bx, img);  // neighbouring tiles share 6 window rows / 8 columns: keep them in one L2
-    const int t = threadIdx.x;
-    int l = 0;
-    while (l + 1 < g.nlevels && bx >= g.lv[l + 1].blur_tile0) ++l;
-    const LevelGeo& L = g.lv[l];
-    const int tile = bx - L.blur_tile0;
-    const int ntx = (L.w + kBlurTX - 1) / kBlurTX;
-    const int ty = tile / ntx, tx = tile - ty * ntx;
-    const int X0 = tx * kBlurTX, Y0 = ty * kBlurTY;
-    int stride;
-    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    // staging: one buffer dwordx4 load per 3 staged dwords (6 slots per row, 2 loads per thread) at 32-bit
-    // offsets, the resource bounded by the level's extent (reads past it return 0, never fault); rows
-    // through reflect-101 only on tiles that reach past the top or bottom; dwords left of column 0 or right
-    // of w-1 are skipped (patched from LDS below)
-    {
-        const bool yb = !(Y0 >= 3 && Y0 - 3 + kBlurWR <= L.h);
-        uint32_t bias;
-        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
-        const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;
-        // 3 staged dwords per slot from one dwordx4 load (6 slots per row)
-        constexpr int NT = (kBlurWR * (kBlurWD / 3) + 255) / 256;
-        static_assert(kBlurWD % 3 == 0, "dword triples per staged row");
-        uint4 raw[NT];
-        uint32_t sh[NT];
-        int dst[NT], xs[NT];
-#pragma unroll
-        for (int k = 0; k < NT; ++k) {
-            const uint32_t slot = (uint32_t)(t + 256 * k);
-            const uint32_t r = slot / (uint32_t)(kBlurWD / 3), d = 3u * (slot - (uint32_t)(kBlurWD / 3) * r);
-            const int x = X0 - 4 + 4 * (int)d;  // image column of the first dword's first byte
-            raw[k] = uint4{0u, 0u, 0u, 0u};
-            sh[k] = 0;
-            dst[k] = -1;
-            xs[k] = x;
-            if (slot < (uint32_t)(kBlurWR * (kBlurWD / 3)) && x < L.w) {
-                int ry = Y0 - 3 + (int)r;
-                if (yb) ry = reflect101c(ry, L.h);
-                const int xl = max(x, 0);  // only the left edge tile's first triple starts left of column 0
-                const uint32_t off = __umul24((uint32_t)ry, stride24) + (uint32_t)xl + bias;
-                sh[k] = off & 3u;
-                raw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off - sh[k], 0, 0));
-                if (x < 0) {  // shift the triple so that word i holds column x + 4 i (word 0 is skipped below)
-                    raw[k] = uint4{0u, raw[k].x, raw[k].y, raw[k].z};
-                }
-                dst[k] = (int)(r * kBlurSD + d);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NT; ++k)
-            if (dst[k] >= 0) {
-                const uint32_t w[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-                    if (xs[k] + 4 * i >= 0 && xs[k] + 4 * i < L.w)
-                        src[dst[k] + i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh[k]);
-            }
-    }
-    const bool left = X0 == 0, right = X0 + kBlurTX + 4 > L.w;
-    if (left || right) {  // patch the reflected columns (sources lie inside the window, never patched)
-        __syncthreads();
-        uint8_t* sb = (uint8_t*)src;
-        constexpr int NP = (kBlurWR * 6 + 255) / 256;
-        uint8_t v[NP];
-        int o[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            v[k] = 0;
-            o[k] = -1;
-            const int i = t + 256 * k;
-            const int r = i / 6, j = i - r * 6;
-            const int x = j < 3 ? j - 3 : L.w + j - 3;  // -3 .. -1, w .. w+2
-            const int c = x - X0 + 4;
-            if (r < kBlurWR && c >= 0 && c < 4 * kBlurWD && ((j < 3 && left) || (j >= 3 && right))) {
-                v[k] = sb[r * 4 * kBlurSD + reflect101(x, L.w) - X0 + 4];
-                o[k] = r * 4 * kBlurSD + c;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            if (o[k] >= 0) sb[o[k]] = v[k];
-    }
-    __syncthreads();
-    auto w4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | (b << 8) | (c << 16) | (d << 24); };
-    // horizontal: (row pair m, group of 4 columns gx): 32 x 16 items, 2 per thread
-#pragma unroll
-    for (int j = 0; j < (kBlurWR / 2) * (kBlurTX / 4) / 256; ++j) {
-        const int it = t + 256 * j, m = it >> 4, gx = it & 15;
-        uint32_t h[2][4];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const uint32_t* q = src + (2 * m + rr) * kBlurSD + gx;
-            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
-            // output i reads window bytes 1 + i .. 7 + i of (d0, d1, d2): the 7 taps spread over the aligned
-            // dwords with shifted byte weights (10 v_dot4 per 4 outputs, no v_alignbyte)
-            h[rr][0] = __builtin_amdgcn_udot4(d1, w4(56, 48, 34, 18), __builtin_amdgcn_udot4(d0, w4(0, 18, 34, 48), 0u, false),
-                                              false);
-            h[rr][1] = __builtin_amdgcn_udot4(
-                d2, w4(18, 0, 0, 0),
-                __builtin_amdgcn_udot4(d1, w4(48, 56, 48, 34), __builtin_amdgcn_udot4(d0, w4(0, 0, 18, 34), 0u, false), false),
-                false);
-            h[rr][2] = __builtin_amdgcn_udot4(
-                d2, w4(34, 18, 0, 0),
-                __builtin_amdgcn_udot4(d1, w4(34, 48, 56, 48), __builtin_amdgcn_udot4(d0, w4(0, 0, 0, 18), 0u, false), false),
-                false);
-            h[rr][3] = __builtin_amdgcn_udot4(d2, w4(48, 34, 18, 0), __builtin_amdgcn_udot4(d1, w4(18, 34, 48, 56), 0u, false),
-                                              false);
-        }
-        *(uint4*)(hor + m * kBlurTX + 4 * gx) = uint4{h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
-                                                       h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16)};
-    }
-    __syncthreads();
-    // vertical: (row quad n2, group gx): tile rows 4 n2 .. 4 n2 + 3 from the 5 interleaved row-pair dwords
-    // P(2 n2) .. P(2 n2 + 4) (rows 4 n2, 4 n2 + 1 use P(0..3), rows 4 n2 + 2, 4 n2 + 3 use P(1..4)): one item
-    // per thread (15 x 16 items), 5 LDS reads per 4 output rows
-    uint8_t* dstimg = blur + (int64_t)img * g.blur_bytes + L.blur_off;
-    auto w2 = [](uint32_t a, uint32_t b) { return __builtin_bit_cast(us2, a | (b << 16)); };
-    constexpr int kPairs = kBlurWR / 2;  // row pairs in hor
-    for (int it = t; it < ((kBlurTY + 3) / 4) * (kBlurTX / 4); it += 256) {
-        const int n2 = it >> 4, gx = it & 15;
-        const int y = Y0 + 4 * n2, x = X0 + 4 * gx;
-        if (y >= L.h || x >= L.w) continue;
-        const int n = 2 * n2;
-        uint4 P[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            P[k] = n + k < kPairs ? *(const uint4*)(hor + (n + k) * kBlurTX + 4 * gx) : uint4{0u, 0u, 0u, 0u};
-        uint32_t out[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint32_t p0 = (&P[h2].x)[c], p1 = (&P[h2 + 1].x)[c], p2 = (&P[h2 + 2].x)[c], p3 = (&P[h2 + 3].x)[c];
-                uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(18, 34), 32768u, false);
-                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(48, 56), a, false);
-                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(48, 34), a, false);
-                a = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(18, 0), a, false);
-                uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), w2(0, 18), 32768u, false);
-                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), w2(34, 48), b, false);
-                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), w2(56, 48), b, false);
-                b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), w2(34, 18), b, false);
-                out[2 * h2] |= (a >> 16) << (8 * c);
-                out[2 * h2 + 1] |= (b >> 16) << (8 * c);
-            }
-        }
-        // rows are padded to a 16-byte pitch, so the dwords never leave the row's allocation; rows past the
-        // tile (the last quad of a 58-row tile) or the level are not stored
-        if (probe == 1) {  // microbench probe: no stores unless the value is impossible
-            if (out[0] == 0x12345678u && out[1] == 0x9abcdef0u) *(uint32_t*)(dstimg + (int64_t)y * L.pitch + x) = out[0];
-            continue;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (4 * n2 + r < kBlurTY && y + r < L.h) *(uint32_t*)(dstimg + (int64_t)(y + r) * L.pitch + x) = out[r];
-    }
-}
-
-// ------------------------------------------------------------------------------- k_describe
-// IC_Angle (ORBextractor.cpp:77-104) + steered BRIEF on the blurred level (:108-147) for every kept
-// keypoint, in the output order of the reference (levels ascending, octree order inside a level).
-// Four keypoints per wavefront, 16 lanes each (row q = lane >> 4 of the wave, sub-lane s = lane & 15);
-// a wave's 4 keypoints are consecutive in one level, so level data stays wave-uniform and the
-// wave-uniform scalar work (fastAtan2, the glibc sincosf replica in f64) is paid once per 4 keypoints.
-//  centroid: the 31 x 31 square as 31 rows x 9 aligned dwords, 18 per lane, all issued before the
-//  first use; per dword, the bytes inside the umax disc as a byte mask, then sum(val) and sum(b * val)
-//  by v_dot4_u32_u8: m10 += u0 * S0 + S1, m01 += v * S0; DPP sums over the 16-lane row.
-//  descriptor: sub-lane s evaluates bits s + 16 i (i = 0..15): 32 rotated samples (the reference's FMA
-//  contraction, cvRound = half-even) from the blurred level; round i's ballot is the 16-bit chunk i of
-//  each row's descriptor, kept by sub-lane i and stored as one u16 per lane.
-// Blocks are remapped XCD-aware: each XCD's L2 receives a contiguous run of waves (consecutive
-// keypoints are spatial neighbours in octree order and share cache lines).
-constexpr int kDescWinRows = 37;  // sample rows cy - 18 .. cy + 18
-
-__device__ __forceinline__ int row16_sum(int v) {  // sum over the lane's 16-lane DPP row
-    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
-    return v;
-}
-
-template <int kDescWaves>
-__global__ __launch_bounds__(64 * kDescWaves) void k_describe(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
-                                                  const uint8_t* __restrict__ ws, const uint8_t* __restrict__ blur,
-                                                  const uint32_t* __restrict__ lvl_kp,
-                                                  const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
-                                                  uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
-                                                  const uint2* __restrict__ mw_tab) {
-    __shared__ float4 s_pat[256];
-    // per (row shift sh, window slot): the byte mask of the umax disc and the dot4 weights of m10
-    __shared__ uint2 s_mw[4][31 * 9];
-    // per wave and keypoint row: the blurred 37 x 37 sample window (rows cy - 18 .. cy + 18), staged with
-    // dwordx4 loads from the dword-aligned column at or left of cx - 18; 48 bytes per window row
-    __shared__ uint4 s_win[kDescWaves][4][kDescWinRows * 3];
-    // XCD-aware remap of the flattened grid: hardware block i runs on XCD i % 8
-    const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
-    const int per = nb >> 3;
-    const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;
-    // wave-uniform: keep the image / block index (and everything derived) in SGPRs
-    const int img = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
-    const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
-    const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
-    const int wv = __builtin_amdgcn_readfirstlane(blk * kDescWaves + (int)(threadIdx.x >> 6));  // wave-uniform
-    // the level tables are read into registers here and stored to LDS only after the pixel loads are
-    // issued: their round trip overlaps the keypoint's, and the barrier before the centroid covers them
-    constexpr int kMwPer = (4 * 31 * 9 + 64 * kDescWaves - 1) / (64 * kDescWaves);
-    float4 pat_r = {};
-    if (threadIdx.x < 256) pat_r = ((const float4*)c_pattern)[threadIdx.x];
-    uint2 mw_r[kMwPer];
-#pragma unroll
-    for (int j = 0; j < kMwPer; ++j) {
-        const int i = threadIdx.x + j * 64 * kDescWaves;
-        mw_r[j] = i < 4 * 31 * 9 ? mw_tab[i] : uint2{0u, 0u};
-    }
-    // wave -> (level, 4-keypoint slot) from the level capacities (host constants), so the keypoint load
-    // does not wait for the octree's per-level counts: the counts, the keypoint and the level tables are
-    // one memory round trip, the pixels the next
-    int l = 0, w0 = 0;
-    {
-        bool go = true;
-#pragma unroll
-        for (int i = 0; i + 1 < kMaxLevels; ++i) {
-            const int wc = (g.lv[i].kp_cap + 3) >> 2;
-            if (go && i + 1 < g.nlevels && wv >= w0 + wc) {
-                w0 += wc;
-                l = i + 1;
-            } else {
-                go = false;
-            }
-        }
-    }
-    const LevelGeo& L = g.lv[l];
-    const int idx = 4 * (wv - w0) + q;  // keypoint of this row inside level l
-    const bool in_cap = idx < L.kp_cap;
-    const uint32_t key = in_cap ? lvl_kp[(int64_t)img * g.lvl_kp_cap + L.kp_off + idx] : 0u;
-    const int* cnt = lvl_count + img * g.nlevels;
-    int pre[kMaxLevels + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int i = 0; i < kMaxLevels; ++i) pre[i + 1] = pre[i] + (i < g.nlevels ? cnt[i] : 0);
-    if (blk == 0 && threadIdx.x == 0) out_count[img] = pre[kMaxLevels];
-    const int n_l = pre[l + 1] - pre[l];
-    const bool valid = in_cap && idx < n_l;
-    const int o = pre[l] + idx;
-    int stride;
-    const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
-    // slots past the level's count hold stale keys: clamp them to where real keypoints lie
-    // ([19, w - 20] x [19, h - 20]) so every row's loads stay inside the level
-    const int cx = min(max((int)(key & 0xFFF), kEdge), L.w - kEdge - 1);
-    const int cy = min(max((int)((key >> 12) & 0xFFF), kEdge), L.h - kEdge - 1);
-    const int score = key >> 24;
-    // ---- intensity centroid: 18 dwords per lane, buffer loads at 32-bit offsets from the level base
-    uint32_t lvl_bias;
-    const __amdgpu_buffer_rsrc_t lr = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &lvl_bias);
-    const uint32_t off0 = (uint32_t)((cy - kHalfPatch) * stride + cx - kHalfPatch) + lvl_bias;
-    const uint32_t stride24 = (uint32_t)stride & 0xFFFFFFu;  // provably 24-bit: v_mul_u32_u24, full rate
-    constexpr int NW = (31 * 9 + 15) / 16;
-    // slot sl + 16 k of the 31 x 9 window -> (row r, dword d), stepped without division (16 = 9 + 7);
-    // recomputed in the second loop rather than kept live across the loads
-    const int r_init = sl >= 9 ? 1 : 0, d_init = sl - 9 * r_init;
-    uint32_t word[NW];
-    {
-        int r = r_init, d = d_init;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            word[k] = 0;
-            if (r < 31) {
-                const uint32_t off = off0 + (uint32_t)(r & 63) * stride24;  // both operands provably 24-bit
-                word[k] = __builtin_amdgcn_raw_buffer_load_b32(lr, (off & ~3u) + 4u * d, 0, 0);
-            }
-            d += 7;
-            r += 1;
-            if (d >= 9) {
-                d -= 9;
-                r += 1;
-            }
-        }
-    }
-    // ---- blurred sample window: 37 rows x 3 dwordx4 = 111 slots, sub-lane sl takes slots sl + 16 k
-    //      (16 = 5 rows + 1 column), loads in flight during the centroid arithmetic
-    const __amdgpu_buffer_rsrc_t br = uniform_rsrc(blur + (int64_t)img * g.blur_bytes + L.blur_off);
-    const uint32_t win0 = (uint32_t)((cy - 18) * L.pitch + ((cx - 18) & ~3));
-    uint4 wv4[7];
-    {
-        int r = sl / 3, c = sl - 3 * (sl / 3);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            wv4[k] = uint4{0u, 0u, 0u, 0u};
-            if (r < kDescWinRows)
-                wv4[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       br, win0 + (uint32_t)r * (uint32_t)L.pitch + 16u * c, 0, 0));
-            r += 5;
-            c += 1;
-            if (c >= 3) {
-                c -= 3;
-                r += 1;
-            }
-        }
-    }
-    if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
-#pragma unroll
-    for (int j = 0; j < kMwPer; ++j) {
-        const int i = threadIdx.x + j * 64 * kDescWaves;
-        if (i < 4 * 31 * 9) (&s_mw[0][0])[i] = mw_r[j];
-    }
-    __syncthreads();  // the level tables (s_mw, s_pat) are in LDS
-    // m10 = sum (u0 + b) val_b, m01 = sum v val_b with non-negative byte weights (u0 + 18 + b), (v + 15)
-    // accumulated by v_dot4 and corrected by -18 / -15 x sum(val); masks and m10 weights from s_mw
-    uint32_t a10 = 0, a01 = 0, a1 = 0;
-    {
-        int r = r_init, d = d_init;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            if (r < 31) {
-                const int sh = (int)((off0 + (uint32_t)(r & 63) * stride24) & 3u);
-                const uint2 mw2 = (&s_mw[0][0])[sh * 279 + ((r & 63) << 3) + (r & 63) + d];
-                const uint32_t mw = word[k] & mw2.x;
-                a10 = __builtin_amdgcn_udot4(mw, mw2.y, a10, false);
-                a01 = __builtin_amdgcn_udot4(mw, __builtin_amdgcn_perm(0u, (uint32_t)r, 0u), a01, false);  // v + 15 = r
-                a1 = __builtin_amdgcn_udot4(mw, 0x01010101u, a1, false);
-            }
-            d += 7;
-            r += 1;
-            if (d >= 9) {
-                d -= 9;
-                r += 1;
-            }
-        }
-    }
-    int m10 = (int)a10 - 18 * (int)a1, m01 = (int)a01 - 15 * (int)a1;
-    m10 = row16_sum(m10);
-    m01 = row16_sum(m01);
-    const float angle = fast_atan2((float)m01, (float)m10);
-    float b, a;
-    glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
-    // ---- steered BRIEF: 32 samples per lane (|offset| <= 13 * sqrt 2 < 18.4, so |rint| <= 18) read from
-    //      the staged window in LDS: window byte (18 + row) * 48 + 18 + col + ((cx - 18) & 3)
-    uint4* win = s_win[threadIdx.x >> 6][q];
-    {
-        int r = sl / 3, c = sl - 3 * (sl / 3);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            if (r < kDescWinRows) win[3 * r + c] = wv4[k];
-            r += 5;
-            c += 1;
-            if (c >= 3) {
-                c -= 3;
-                r += 1;
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // rint by the 1.5 * 2^23 trick: the sum's low mantissa bits hold 0x400000 + rint(x); v_mad_u32_u24
-    // reads only the low 24 bits, and the biases fold into one per-keypoint constant (mod 2^32)
-    const uint8_t* wb = (const uint8_t*)win;
-    const uint32_t woff = 18u * 48u + 18u + (uint32_t)((cx - 18) & 3) - 0x400000u * 48u - __float_as_uint(12582912.0f);
-    int val[32];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float4 pt = s_pat[sl + 16 * i];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
-            // (row, col) = (fma(px, b, py a), fma(px, a, -(py b))) as packed f32: v_pk_mul + v_pk_fma + v_pk_add,
-            // each half rounded exactly like the scalar expression
-            const df2 m = (df2){py, py} * (df2){a, -b};
-            const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, m) + (df2){12582912.0f, 12582912.0f};
-            const uint32_t fr = __float_as_uint(rc.x), fc = __float_as_uint(rc.y);
-            val[2 * i + e] = wb[(fr & 0xFFFFFFu) * 48u + fc + woff];
-        }
-    }
-    uint64_t mine = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint64_t m = __ballot(val[2 * i] < val[2 * i + 1]);
-        mine = sl == i ? m : mine;
-    }
-    if (valid) {
-        *(uint16_t*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 2 * sl) = (uint16_t)(mine >> (16 * q));
-        if (sl == 0) {
-            orbfe_keypoint kp;
-            kp.x = l ? __fmul_rn((float)cx, L.scale) : (float)cx;
-            kp.y = l ? __fmul_rn((float)cy, L.scale) : (float)cy;
-            kp.size = L.size;
-            kp.angle = angle;
-            kp.response = (float)score;
-            kp.octave = l;
-            out_kp[(int64_t)img * g.kp_cap + o] = kp;
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------- k_orb
@@ -2440,34 +2022,6 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
     }
     hipLaunchKernelGGL(k_octree, dim3(n_images, g.nlevels), dim3(kOctThreads), lds, s, g, cells, cell_count, slots, kd, kn,
                        lvl_kp, lvl_count, overflow, maxcell, variant, prof);
-    return hipGetLastError();
-}
-
-hipError_t launch_blur(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* blur, int n_images,
-                       hipStream_t s, int probe) {
-    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, n_images), dim3(256), 0, s, g, in, in_pitch, ws, blur, probe);
-    return hipGetLastError();
-}
-
-template <int NW>
-static void launch_describe_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
-                               const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
-                               int* out_count, const uint32_t* mw, int n_images, hipStream_t s) {
-    int waves = 0;  // most waves an image can need: 4 keypoints per wave, per level
-    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + 3) / 4;
-    hipLaunchKernelGGL(k_describe<NW>, dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws,
-                       blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, (const uint2*)mw);
-}
-
-// variant: waves per workgroup, 4 or 8 (0 = production: 8 — two 512-thread workgroups per CU hold 16 waves,
-// where the 41 KiB of LDS of a 4-wave workgroup allow 12; measured 866 -> 790 us per 256 pairs)
-hipError_t launch_describe(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint8_t* blur,
-                           const uint32_t* lvl_kp, const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc,
-                           int* out_count, const uint32_t* mw, int n_images, hipStream_t s, int variant) {
-    if (variant == 4)
-        launch_describe_nw<4>(g, in, in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, mw, n_images, s);
-    else
-        launch_describe_nw<8>(g, in, in_pitch, ws, blur, lvl_kp, lvl_count, out_kp, out_desc, out_count, mw, n_images, s);
     return hipGetLastError();
 }
 

@@ -162,7 +162,7 @@ def test_stereo_configurations_match_restatement(ci):
 def test_batch_path_misaligned_images(wh):
     """Odd W*H: every second image of a (2P, H, W) batch starts at an address that is not 4-byte aligned
     (and so does the whole batch when it is a slice starting at an odd image).  The buffer loads of
-    k_blur / k_describe / k_stereo must re-align from the dword at or below the image base; results equal
+    k_resize / k_detect / k_orb / k_stereo must re-align from the dword at or below the image base; results equal
     the single-image path, whose staging buffer is aligned."""
     torch = pytest.importorskip("torch")
     from pyorbslam_amd.batch import StereoFrontEnd
@@ -302,7 +302,7 @@ def test_default_bench_configuration_sampled():
     P, S = 512, 4
     host = synth.make_batch(P, seed0=0)
     images = torch.from_numpy(host).cuda()
-    fes = [StereoFrontEnd(max_pairs=P // S, lanes=1, blur_fork=False) for _ in range(S)]
+    fes = [StereoFrontEnd(max_pairs=P // S, lanes=1) for _ in range(S)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     for _ in range(2):  # the bench repeats the step on the same buffers
         for i, (f, st) in enumerate(zip(fes, streams)):
