@@ -121,8 +121,6 @@ struct orbfe_ctx {
     ~orbfe_ctx() {
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
-        for (int k = 0; k <= kLanes; ++k) {
-        }
         for (int k = 0; k < kLanes; ++k) {
             if (lane_stream[k]) (void)hipStreamDestroy(lane_stream[k]);
             if (lane_done[k]) (void)hipEventDestroy(lane_done[k]);
