@@ -4,28 +4,44 @@
 Default (--mode throughput), the BASELINE.json metric:
   One step = one pass of the whole hot path over one batch of P synthetic stereo pairs resident in HBM
   (pyramid -> FAST cells -> octree -> IC angle + blur + rBRIEF for both images -> stereo match), as S
-  independent handles of P/S pairs on S streams.  N GPUs: one process per GPU (torch.distributed.run),
-  every rank processes its own P pairs (pairs are independent: weak scaling, no data-path collective);
-  timing = barrier + synchronize on both sides of exactly K steps, max over ranks;
-  value = N * P * K / max_elapsed.
-  After the timed region (untimed): every handle's overflow word is read and the first and last pair of
-  every handle are compared bit for bit with the oracle (parity on the bench's own workload); then a
-  standalone pass runs the same P pairs as ONE handle on ONE stream with HIP events around each stage,
-  which gives every stage's own duration for the roofline (no other handle's kernels overlap it).
-  --gather adds a timed device-side gather of every pair's packed results to rank 0 (RCCL).
+  independent handles of P/S pairs on S streams.  N GPUs: one process per GPU, every rank processes its
+  own P pairs (pairs are independent: weak scaling, no data-path collective); timing = barrier +
+  synchronize on both sides of exactly K steps, max over ranks; value = N * P * K / max_elapsed.
+  --total-pairs T: strong scaling instead (config C4 is `--gpus 8 --total-pairs 64`): the T pairs are
+  sharded over the ranks (dist.shard), value = T * K / max_elapsed.
 
---mode frame: BASELINE config C3, the per-frame drop-in path (Tracking's calls per frame: Frame
-  construction with the pair-batched ExtractORB / stereo, search_by_projection_f_f, _f_p) over the
-  synthetic moving sequence of tests/golden/sequence_kitti_synth.npz, bit-exact against it, reported as
-  frames/s and per-frame latency next to the reference's per-frame CPU time.
+  Launch: `python bench.py --gpus N` with N > 1 and no torch.distributed environment starts N ranks as
+  fresh child processes (torch.distributed.run, before this process makes any GPU call) and exits with
+  their status; under torchrun, WORLD_SIZE must equal --gpus (exit 2 otherwise).
+
+  Beside `value` (never replacing it), each untimed or separately timed:
+  * parity of the bench's own workload: every handle's overflow word, first / last pair of every handle
+    bit for bit against the oracle extractor and the stereo restatement;
+  * with_gather (N > 1): k_pack of every pair's record + one RCCL gather to rank 0, timed like a step;
+  * c4_strong: the C4 configuration (64 pairs in total, sharded over the N ranks) timed like a step, plus
+    its gather when N > 1, so every N of the driver's scaling run records the C4 curve;
+  * host_fed: the same P pairs streamed from pinned host memory every step (H2D on a copy stream, double
+    buffered against compute; packed records D2H), the PCIe-inclusive rate (stereo_kitti.py:39-47 reads
+    images on the host);
+  * a standalone pass (the same P pairs as ONE handle on ONE stream, HIP events around each stage) that
+    gives every stage's own duration for the roofline; PMC-derived figures (traffic, VALU instructions)
+    are taken from profiles/*.json only when they were measured on the loaded library's build id;
+  * c3_frame (N = 1): BASELINE config C3, the per-frame drop-in tracking loop over the recorded synthetic
+    sequence, bit-exact against its golden, p50 latency per frame;
+  * cpu_baseline (N = 1, before any GPU call): the reference's CPU path as restated by the oracle.
+
+--mode frame: C3 alone as its own JSON line.
 
 Prints ONE JSON line on rank 0 (fields: DESIGN.md §5).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,13 +51,21 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4  # wave64 VALU issue, all SIMDs at the 2.4 GHz peak clock
+# wave64 VALU issue peak of the instruction class these kernels are made of: 4 cycles per wave64
+# instruction per SIMD (packed 16-bit, dot2/dot4, perm, sad, alignbyte, shifts, integer multiply, max3 —
+# ~70 % of their static VALU mix), 256 CUs x 4 SIMDs at the 2.4 GHz peak clock.  Measured per instruction:
+# profiles/r03/mulrate_r3b.log (tools/dbg/mulrate.hip); the add / logic / mov / f32 add-mul class issues
+# at ~2.4 cycles, so a kernel made only of those could exceed this figure.
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4
+VALU_PEAK_FAST_CLASS_GIPS = 256 * 4 * 2.4 / 2.4
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-STAGES = ["resize", "detect", "octree", "blur", "describe", "stereo"]
-STAGE_KERNELS = {"resize": "k_resize (x7 levels)", "detect": "k_detect", "octree": "k_octree", "blur": "(fused in k_orb)",
+PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16 spec, per direction
+STAGES = ["resize", "detect", "octree", "describe", "stereo"]  # orbfe_profile_read order (ORBFE_NSTAGES)
+STAGE_KERNELS = {"resize": "k_resize (x7 levels)", "detect": "k_detect", "octree": "k_octree",
                  "describe": "k_orb (IC angle + per-keypoint 7x7 blur + steered BRIEF)",
                  "stereo": "k_stereo_bucket + k_stereo"}
 CAMERAS = {(1241, 376): ("kitti", "KITTI 1241x376"), (752, 480): ("euroc", "EuRoC 752x480")}
+C4_TOTAL_PAIRS = 64    # BASELINE.json configs[3]
 
 
 def level_sizes(W, H, nlevels=8, sf=1.2):
@@ -64,16 +88,19 @@ def algorithmic_bytes_per_pair(W, H, N=2000, nlevels=8):
         "detect": 2 * px,
         # the selected keypoints (4 B packed) written and read back
         "octree": 2 * 2 * N * 4,
-        # fused into k_orb: no blurred level is written or read (kept as a 0-ms stage for the JSON layout)
-        "blur": 0,
         # k_orb: each level's pixels around the keypoints (at most the level, read once) + the keypoint
-        # records and descriptors written (24 + 32 B per keypoint)
+        # records and descriptors written (24 + 32 B per keypoint); the 7x7 blur is computed per keypoint
         "describe": 2 * (px + N * 56),
         # both keypoint sets read + uR/depth written
         "stereo": 2 * N * 56 + N * 8,
     }
     total = 2 * (px + derived + 2 * N * 56) + N * 8
     return total, per_stage
+
+
+def shard(n, world, rank):
+    base, extra = divmod(n, world)
+    return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
 
 # ------------------------------------------------------------------------------------------- cpu baseline
@@ -137,7 +164,6 @@ def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, pro
     else:
         out["value"] = out["value_1core"]
         allp = ""
-    ratio = None
     f = ROOT / "profiles" / "cpu_ratio.json"
     if f.exists():
         ratio = json.loads(f.read_text())
@@ -151,7 +177,7 @@ def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, pro
 
 
 # ------------------------------------------------------------------------------------------ parity check
-def parity_check(fes, host, per, width, height, nfeatures):
+def parity_check(fes, counts, host, width, height, nfeatures):
     """First and last pair of every handle against the oracle extractor and the stereo restatement, bit for
     bit; every handle's overflow word.  Returns (pairs checked, max overflow word, failures)."""
     from oracle import stereo_oracle
@@ -161,10 +187,11 @@ def parity_check(fes, host, per, width, height, nfeatures):
     checked, ovf, bad = 0, 0, []
     oL, oR = OracleExtractor(nfeatures=nfeatures), OracleExtractor(nfeatures=nfeatures)
     t = oL.tables()
-    for hi, f in enumerate(fes):
+    first = 0
+    for hi, (f, n) in enumerate(zip(fes, counts)):
         ovf = max(ovf, f.overflow())
-        for p in sorted({0, per - 1}):
-            g = hi * per + p  # global pair index inside this rank's batch
+        for p in sorted({0, n - 1}) if n else []:
+            g = first + p  # pair index inside this rank's batch
             L, R = host[2 * g], host[2 * g + 1]
             kl, dl = oL.extract(L)
             kr, dr = oR.extract(R)
@@ -185,14 +212,16 @@ def parity_check(fes, host, per, width, height, nfeatures):
                     bad.append(f"handle {hi} pair {p}: stereo differs from the restatement")
                     break
             checked += 1
+        first += n
     return checked, ovf, bad
 
 
 # ---------------------------------------------------------------------------------------------- frame mode
-def frame_mode(args):
-    """C3: the per-frame drop-in path over the recorded synthetic sequence (tests/seq_harness.py)."""
+def run_c3(steps: int, warmup: int) -> dict:
+    """C3: the per-frame drop-in path over the recorded synthetic sequence (tests/seq_harness.py), bit-exact
+    against its golden while timed."""
     import torch
-    assert torch.cuda.is_available(), "--mode frame needs a GPU"
+    assert torch.cuda.is_available(), "C3 needs a GPU"
     sys.path.insert(0, str(ROOT / "tests"))
     import seq_harness as H
     from pyorbslam_amd import frame as F
@@ -213,17 +242,14 @@ def frame_mode(args):
 
     F.install(DropInFrame)
     ex = (ORBextractor(**H.PARAMS), ORBextractor(**H.PARAMS))
-    for _ in range(max(args.warmup, 1)):
+    for _ in range(max(warmup, 1)):
         H.replay(g, Cached(), ex, ORBMatcher, DropInFrame, n_frames=3)
-    reps = max(1, args.steps // meta["n_frames"]) if args.steps >= meta["n_frames"] else 1
+    reps = max(1, steps // meta["n_frames"]) if steps >= meta["n_frames"] else 1
     timer, bad = {}, []
     t0 = time.perf_counter()
     for _ in range(reps):
         bad += H.replay(g, Cached(), ex, ORBMatcher, DropInFrame, timer=timer)
     wall = time.perf_counter() - t0
-    if bad:
-        print(json.dumps({"error": "frame-mode parity failure", "details": bad[:10]}), flush=True)
-        raise SystemExit(2)
     fr, ff, fp = (np.array(timer[k]) for k in ("frame", "f_f", "f_p"))
     lat = fr + ff + fp
     nfr = len(lat)
@@ -233,16 +259,13 @@ def frame_mode(args):
     if rf.exists():
         ref_ext = json.loads(rf.read_text())["oracle_extract_s_per_pair"]
     ref_frame = (ref_ext or 0.0) + ref["stereo"] + ref["grid"] + ref["f_f"] + ref["f_p"]
-    out = {
-        "metric": "frames/s (C3 per-frame drop-in: Frame(L,R) extract+stereo+grid, search_by_projection_f_f, _f_p)",
-        "value": round(nfr / float(lat.sum()), 3), "unit": "frames/s", "n_gpus": 1, "steps": nfr, "warmup": args.warmup,
-        "ms_per_step": round(1e3 * float(lat.mean()), 3), "higher_is_better": True, "scaling": "none",
-        "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic moving stereo sequence (pyorbslam_amd.synth.StereoSequence seed 0), recorded map-point "
-                "inputs of tests/golden/sequence_kitti_synth.npz",
-        "config": {"workload": f"kitti{meta['width']}x{meta['height']}_seq{meta['n_frames']}f_2000f_tracking",
-                   "frames": meta["n_frames"], "repeats": reps, "nfeatures": 2000},
-        "parity": f"bit-exact vs the reference tracking-loop golden on all {nfr} frames",
+    return {
+        "frames_per_s": round(nfr / float(lat.sum()), 3), "frames": nfr, "repeats": reps,
+        "mean_ms": round(1e3 * float(lat.mean()), 3),
+        "workload": f"kitti{meta['width']}x{meta['height']}_seq{meta['n_frames']}f_2000f_tracking",
+        "parity": (f"bit-exact vs the reference tracking-loop golden on all {nfr} frames" if not bad
+                   else f"FAILED: {bad[:5]}"),
+        "parity_ok": not bad,
         "latency_ms": {"p50": round(1e3 * float(np.median(lat)), 3), "p90": round(1e3 * float(np.percentile(lat, 90)), 3),
                        "max": round(1e3 * float(lat.max()), 3),
                        "frame_ctor_p50": round(1e3 * float(np.median(fr)), 3),
@@ -252,8 +275,217 @@ def frame_mode(args):
         "reference_cpu_s_per_frame": {"extract_LR_oracle_cpp": ref_ext, **{k: round(v, 5) for k, v in ref.items()},
                                       "total": round(ref_frame, 4), "host": meta["reference_timing_host"]},
         "speedup_vs_reference_frame": round(ref_frame / float(lat.mean()), 2),
+        "what": "Frame(L,R) (pair-batched ExtractORB + stereo + grid), search_by_projection_f_f, _f_p per frame; "
+                "recorded map-point inputs of tests/golden/sequence_kitti_synth.npz",
+    }
+
+
+def frame_mode(args):
+    c3 = run_c3(args.steps, args.warmup)
+    if not c3["parity_ok"]:
+        print(json.dumps({"error": "frame-mode parity failure", "details": c3["parity"]}), flush=True)
+        raise SystemExit(2)
+    out = {
+        "metric": "frames/s (C3 per-frame drop-in: Frame(L,R) extract+stereo+grid, search_by_projection_f_f, _f_p)",
+        "value": c3["frames_per_s"], "unit": "frames/s", "n_gpus": 1, "steps": c3["frames"], "warmup": args.warmup,
+        "ms_per_step": c3["mean_ms"], "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic moving stereo sequence (pyorbslam_amd.synth.StereoSequence seed 0), recorded map-point "
+                "inputs of tests/golden/sequence_kitti_synth.npz",
+        "config": {"workload": c3["workload"], "frames": c3["frames"], "repeats": c3["repeats"], "nfeatures": 2000},
+        **{k: c3[k] for k in ("parity", "latency_ms", "wall_s_incl_checks", "reference_cpu_s_per_frame",
+                              "speedup_vs_reference_frame")},
     }
     print(json.dumps(out), flush=True)
+
+
+# --------------------------------------------------------------------------------------- launch / ranks
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) outside torchrun: start N ranks as fresh child processes through
+    torch.distributed.run and return their exit status.  This process makes no GPU call (device_count
+    does not initialise the GPU on this image), so no GPU context exists when the children start."""
+    import torch
+    backend = os.environ.get("ORBFE_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < args.gpus:
+        print(json.dumps({"error": f"--gpus {args.gpus} needs {args.gpus} GPUs for one RCCL rank each; this host "
+                                   f"shows {ndev} (ORBFE_DIST_BACKEND=gloo rehearses several ranks on one GPU)"}),
+              flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args) -> tuple[int, int, int] | None:
+    """(world, rank, local rank) of this process, or None when it must launch the ranks itself.  Exits 2
+    when a torch.distributed environment disagrees with --gpus."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(json.dumps({"error": f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
+                                       f"{world}-rank run as {args.gpus} GPUs"}), flush=True)
+            raise SystemExit(2)
+        return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1:
+        return None
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    return 1, 0, 0
+
+
+# ------------------------------------------------------------------------------------------ the workload
+class Shard:
+    """This rank's pairs as S handles on S streams (pairs split evenly, dist.shard), each enqueue of the
+    whole front-end on its own stream so that the latency-bound stages of one overlap the issue-bound
+    stages of another; every pair is processed exactly once per step."""
+
+    def __init__(self, images, n_pairs, streams, dev, width, height, nfeatures, lanes=1):
+        import torch
+        from pyorbslam_amd.batch import StereoFrontEnd
+        S = max(1, min(streams, n_pairs))
+        self.counts = [shard(n_pairs, S, i)[1] for i in range(S)]
+        self.fes = [StereoFrontEnd(width, height, max_pairs=max(c, 1), nfeatures=nfeatures, lanes=lanes)
+                    for c in self.counts]
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+        self.subs, o = [], 0
+        for c in self.counts:
+            self.subs.append(images[2 * o: 2 * (o + c)])
+            o += c
+        self.n_pairs = n_pairs
+
+    def step(self, subs=None):
+        from pyorbslam_amd.batch import KITTI_BF, KITTI_FX
+        for f, st, sub, c in zip(self.fes, self.streams, subs or self.subs, self.counts):
+            if c:
+                f.enqueue(sub, c, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
+
+
+def timed(fn, steps, warmup, dev, world):
+    """warmup untimed calls, then exactly `steps` calls bracketed by barrier + synchronize on both sides;
+    max over ranks of the elapsed seconds."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks(elapsed, dev, world)
+
+
+def max_over_ranks(v, dev, world):
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    t = t.to(dev) if dist.get_backend() == "nccl" else t
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
+    """The shard's pairs streamed from pinned host memory every step: H2D of the images on a copy stream
+    into one of two device buffers while the handles compute on the other; after its batch each handle
+    packs its pairs' records (k_pack) and a second copy stream brings them back D2H into pinned memory.
+    Timed like a step (barrier + synchronize, max over ranks).  The records of the last step are checked
+    against the handles' own results."""
+    import torch
+    from pyorbslam_amd import dist as D
+    from pyorbslam_amd._lib import call
+    n = sh.n_pairs
+    hin = torch.from_numpy(host).pin_memory()
+    dbuf = [torch.empty(hin.shape, dtype=torch.uint8, device=dev) for _ in range(2)]
+    rb = D.record_bytes(sh.fes[0].kp_cap)
+    drec = [torch.empty((n, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
+    hrec = [torch.empty((n, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_free = [[torch.cuda.Event() for _ in sh.fes] for _ in range(2)]   # handle j done reading dbuf[b]
+    ev_out = [torch.cuda.Event() for _ in range(2)]                      # D2H of drec[b] done
+    it = [0]
+    used = [[False, False], [False, False]]  # [b][0]: ev_free recorded, [b][1]: ev_out recorded
+
+    def step():
+        b = it[0] % 2
+        it[0] += 1
+        with torch.cuda.stream(h2d):
+            if used[b][0]:
+                for e in ev_free[b]:
+                    h2d.wait_event(e)
+            dbuf[b].copy_(hin, non_blocking=True)
+            ev_in[b].record(h2d)
+        subs, o = [], 0
+        for c in sh.counts:
+            subs.append(dbuf[b][2 * o: 2 * (o + c)])
+            o += c
+        o = 0
+        for j, (f, st, sub, c) in enumerate(zip(sh.fes, sh.streams, subs, sh.counts)):
+            st.wait_event(ev_in[b])
+            if used[b][1]:
+                st.wait_event(ev_out[b])   # drec[b] of two steps ago has left the device
+            f.enqueue(sub, c, stream_ptr=st.cuda_stream)
+            call("orbfe_batch_pack_device", f.handle, C.c_void_p(drec[b][o].data_ptr()), rb, 0, c,
+                 C.c_void_p(st.cuda_stream))
+            ev_free[b][j].record(st)
+            o += c
+        used[b][0] = True
+        with torch.cuda.stream(d2h):
+            for e in ev_free[b]:
+                d2h.wait_event(e)
+            hrec[b].copy_(drec[b], non_blocking=True)
+            ev_out[b].record(d2h)
+        used[b][1] = True
+
+    el = timed(step, steps, warmup, dev, world)
+    last = (it[0] - 1) % 2
+    u = D.unpack(sh.fes[0].kp_cap, hrec[last][0].numpy())
+    k, d = sh.fes[0].fetch_image(0)
+    s = sh.fes[0].fetch_stereo(0)
+    ok = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
+          and np.array_equal(u["u_right"], s["u_right"]))
+    if not ok:
+        raise RuntimeError("host-fed record of pair 0 differs from the handle's own results")
+    in_b = host.nbytes
+    out_b = n * rb
+    pps = world * n * steps / el
+    return {"value": round(pps, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "h2d_bytes_per_pair": int(in_b // n), "d2h_bytes_per_pair": int(rb),
+            "h2d_GBs_per_gpu": round(in_b * steps / el / 1e9, 2), "d2h_GBs_per_gpu": round(out_b * steps / el / 1e9, 2),
+            "pcie_bound_pairs_per_s_per_gpu": round(PCIE_PEAK_GBS * 1e9 / (in_b / n), 1),
+            "record_check": ok,
+            "what": "images H2D from pinned host memory every step (copy stream, two device buffers) overlapped "
+                    "with compute, every pair's packed record D2H into pinned memory (second copy stream); "
+                    "PCIe Gen5 x16 spec 63 GB/s per direction bounds the H2D leg"}
+
+
+# ----------------------------------------------------------------------------------- evidence lookups
+def stamped(name: str, key: str, build: str):
+    """profiles/<name>.json entry `key` if it was measured on library build `build`, else (None, reason)."""
+    f = ROOT / "profiles" / name
+    if not f.exists():
+        return None, f"profiles/{name} absent"
+    data = json.loads(f.read_text())
+    if key not in data:
+        return None, f"no {key} entry in profiles/{name}"
+    meta = data.get(key + "_meta", {})
+    if meta.get("build_id") != build:
+        return None, (f"profiles/{name} {key} was measured on build {meta.get('build_id', 'unstamped')}, "
+                      f"the loaded library is {build}: dropped")
+    return data[key], f"profiles/{name} {key} (build {build}, git {meta.get('git_rev', '?')})"
 
 
 # --------------------------------------------------------------------------------------------------- main
@@ -263,7 +495,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--pairs", type=int, default=512, help="stereo pairs per step per GPU (256: -1.7 %%, tools/dbg/pairs_sweep.sh)")
+    ap.add_argument("--pairs", type=int, default=512, help="stereo pairs per step per GPU (weak scaling)")
+    ap.add_argument("--total-pairs", type=int, default=0,
+                    help="strong scaling: this many pairs per step in total, sharded over the GPUs (C4: 64)")
     ap.add_argument("--width", type=int, default=1241)
     ap.add_argument("--height", type=int, default=376)
     ap.add_argument("--nfeatures", type=int, default=2000)
@@ -279,18 +513,22 @@ def main():
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the standalone per-stage pass (for rocprofv3 --pmc runs whose dispatches must all be "
                          "standalone)")
-    ap.add_argument("--gather", action="store_true",
-                    help="also time a device-side gather of every pair's packed results to rank 0 (RCCL)")
+    ap.add_argument("--no-gather", action="store_true", help="skip the timed rank-0 gather (N > 1)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 (64 pairs in total) line")
+    ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed (PCIe-inclusive) line")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 tracking-loop latency (N = 1)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    wr = check_world(args)
+    if wr is None:
+        raise SystemExit(launch_ranks(args))
+    world, rank, local = wr
     if args.mode == "frame":
         frame_mode(args)
         return
+    extras = not args.roofline_only
     cpu = None
-    if world == 1 and args.cpu_sample > 0 and not args.roofline_only:
+    if world == 1 and args.cpu_sample > 0 and extras:
         try:
             share = len(os.sched_getaffinity(0))
         except AttributeError:  # pragma: no cover
@@ -303,67 +541,44 @@ def main():
 
     # one process per GPU; the modulo only matters when rehearsing several ranks on one GPU (gloo)
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(dev)
         backend = os.environ.get("ORBFE_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
 
-    from pyorbslam_amd import synth
-    from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
+    from pyorbslam_amd import _lib, synth
+    from pyorbslam_amd import dist as D
     from pyorbslam_amd._lib import call
-    import ctypes as C
+    from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
 
-    P = args.pairs
-    S = max(1, args.streams)
-    if P % S:
-        raise SystemExit("--pairs must be a multiple of --streams")
-    host = synth.make_batch(P, seed0=rank * P, width=args.width, height=args.height)
+    strong = args.total_pairs > 0
+    if strong:
+        first, P = shard(args.total_pairs, world, rank)
+        total = args.total_pairs
+    else:
+        first, P = rank * args.pairs, args.pairs
+        total = world * args.pairs
+    host = synth.make_batch(P, seed0=first, width=args.width, height=args.height)
     images = torch.from_numpy(host).to(dev)
-    per = P // S
     elapsed = None
-    fes = []
-    if not args.roofline_only:
-        # S sub-batches of P/S pairs, each with its own handle (buffers) and stream, so that the latency-bound
-        # stages of one overlap the issue-bound stages of another; every pair is still processed exactly once
-        fes = [StereoFrontEnd(args.width, args.height, max_pairs=per, nfeatures=args.nfeatures, lanes=args.lanes) for _ in range(S)]
-        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-        subs = [images[2 * per * i: 2 * per * (i + 1)] for i in range(S)]
-
-        def step():
-            for f, st, sub in zip(fes, streams, subs):
-                f.enqueue(sub, per, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
-
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64)
-            t = t.to(dev) if dist.get_backend() == "nccl" else t
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+    sh = None
+    n_handles = 0
+    if extras:
+        sh = Shard(images, P, args.streams, dev, args.width, args.height, args.nfeatures, args.lanes)
+        n_handles = len(sh.fes)
+        elapsed = timed(sh.step, args.steps, args.warmup, dev, world)
 
     gather = None
-    if args.gather and fes:
-        from pyorbslam_amd import dist as D
-        gather = D.timed_gather(fes, per, dev, world, rank, reps=3)
+    if extras and world > 1 and not args.no_gather:
+        gather = D.timed_gather(sh.fes, sh.counts, dev, world, rank, max_local=shard(total, world, 0)[1])
 
     # ---- parity of the bench's own workload (untimed)
     parity = None
-    if fes and not args.no_parity:
-        checked, ovf, bad = parity_check(fes, host, per, args.width, args.height, args.nfeatures)
+    if sh is not None and not args.no_parity:
+        checked, ovf, bad = parity_check(sh.fes, sh.counts, host, args.width, args.height, args.nfeatures)
         if world > 1:
             t = torch.tensor([len(bad), ovf, checked], dtype=torch.int64)
             t = t.to(dev) if dist.get_backend() == "nccl" else t
@@ -378,10 +593,31 @@ def main():
                                   "details": bad[:10]}), flush=True)
             raise SystemExit(3)
 
+    # ---- C4: 64 pairs in total sharded over the ranks, timed like a step (+ its gather when N > 1)
+    c4 = None
+    if extras and not strong and not args.no_c4:
+        c4_first, c4_n = shard(C4_TOTAL_PAIRS, world, rank)
+        c4_sh = Shard(images[: 2 * c4_n], c4_n, args.streams, dev, args.width, args.height, args.nfeatures)
+        el4 = timed(c4_sh.step, args.steps, args.warmup, dev, world)
+        c4 = {"total_pairs": C4_TOTAL_PAIRS, "pairs_per_gpu": c4_n, "handles_per_gpu": len(c4_sh.fes),
+              "value": round(C4_TOTAL_PAIRS * args.steps / el4, 2), "unit": "pairs/s",
+              "ms_per_step": round(el4 / args.steps * 1e3, 4), "scaling": "strong",
+              "what": "BASELINE configs[3]: 64 synthetic pairs per step in total, sharded over the ranks (dist.shard), "
+                      "barrier + synchronize around K steps, max over ranks"}
+        if world > 1 and not args.no_gather:
+            c4["with_gather"] = D.timed_gather(c4_sh.fes, c4_sh.counts, dev, world, rank,
+                                               max_local=shard(C4_TOTAL_PAIRS, world, 0)[1])
+        del c4_sh
+
+    # ---- host-fed (PCIe-inclusive) rate of the same workload
+    hf = None
+    if extras and not args.no_host_fed:
+        hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2)
+
     # ---- standalone per-stage pass: the same P pairs as one handle on one stream, HIP events per stage
     stage_ms = {}
     if args.roofline_steps > 0 and rank == 0:
-        del fes
+        del sh
         torch.cuda.synchronize(dev)
         solo = StereoFrontEnd(args.width, args.height, max_pairs=P, nfeatures=args.nfeatures, lanes=1)
         st0 = torch.cuda.current_stream(dev)
@@ -395,34 +631,45 @@ def main():
         nb = C.c_int32()
         call("orbfe_profile_read", solo.handle, ms, C.byref(nb))
         stage_ms = {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
+        del solo
+
+    c3 = None
+    if extras and world == 1 and not args.no_c3 and (ROOT / "tests" / "golden" / "sequence_kitti_synth.npz").exists():
+        c3 = run_c3(32, 1)
+        if not c3["parity_ok"]:
+            print(json.dumps({"error": "C3 tracking-loop parity failure", "details": c3["parity"]}), flush=True)
+            raise SystemExit(3)
 
     if rank == 0:
+        build = _lib.build_id()
         total_b, per_stage_b = algorithmic_bytes_per_pair(args.width, args.height, args.nfeatures)
         cam, cam_name = CAMERAS.get((args.width, args.height), ("custom", f"{args.width}x{args.height}"))
-        workload = f"{cam}{args.width}x{args.height}_synth_{args.nfeatures}f_{P}pairs"
-        tr = None
-        f = ROOT / "profiles" / "traffic.json"
-        if f.exists():
-            tr = json.loads(f.read_text()).get(workload + "_standalone")
+        workload = (f"{cam}{args.width}x{args.height}_synth_{args.nfeatures}f_"
+                    + (f"{args.total_pairs}pairs_total" if strong else f"{P}pairs"))
         out = {"metric": f"stereo pairs/s (ORB extract L+R + stereo match), {cam_name}, 1/2/4/8 GPU"}
         if elapsed is not None:
-            pairs_per_s = world * P * args.steps / elapsed
+            pairs_per_s = total * args.steps / elapsed
             out.update({"value": round(pairs_per_s, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
                         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4)})
         else:
             pairs_per_s = None
             out.update({"value": None, "unit": "pairs/s", "n_gpus": world, "steps": 0, "warmup": 0})
         out.update({
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded band-limited noise + rectangles, right = per-row-block disparity shift)",
-            "config": {"workload": workload, "pairs_per_step_per_gpu": P, "width": args.width, "height": args.height,
+            "config": {"workload": workload, "pairs_per_step_per_gpu": P, "total_pairs_per_step": total,
+                       "width": args.width, "height": args.height,
                        "nfeatures": args.nfeatures, "nlevels": 8, "scaleFactor": 1.2, "iniThFAST": 20, "minThFAST": 7,
-                       "parallelism": f"pairs sharded {world}-way (independent replicas, no data-path collective)",
-                       "handles_per_gpu": S, "lanes_per_handle": args.lanes},
+                       "parallelism": (f"{total} pairs sharded {world}-way" if strong else
+                                       f"{P} pairs per GPU on {world} GPU(s)")
+                       + " (independent ranks, no data-path collective)",
+                       "handles_per_gpu": n_handles, "lanes_per_handle": args.lanes},
+            "build_id": build,
         })
         if parity is not None:
             out.update(parity)
         if stage_ms:
+            tr, tr_src = stamped("traffic.json", workload + "_standalone", build)
             dom = max(stage_ms, key=stage_ms.get)
             ach = {s: per_stage_b[s] * P / (stage_ms[s] * 1e-3) / 1e9 for s in STAGES
                    if stage_ms[s] > 0 and per_stage_b[s] > 0}
@@ -430,7 +677,7 @@ def main():
             out["roofline"] = {
                 "bound": "hbm", "kernel": STAGE_KERNELS[dom], "stage": dom, "achieved": round(ach[dom], 3),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach[dom] / HBM_PEAK_GBS, 6),
-                "traffic": (tr or {}).get(dom),
+                "traffic": (tr or {}).get(dom), "traffic_source": tr_src,
                 "measured": f"standalone pass: {P} pairs as one handle on one stream, HIP events around each stage, "
                             f"mean of {args.roofline_steps} steps (rocprof trace: the {2 * P}-image dispatches)",
                 "algorithmic_bytes_per_pair": per_stage_b[dom], "pipeline_bytes_per_pair": total_b,
@@ -441,23 +688,33 @@ def main():
                                      for s in ach}
             # the bound these kernels actually meet: VALU issue (wave-instructions per step from
             # SQ_INSTS_VALU over the same standalone pass, profiles/valu.json, tools/valu.py)
-            vf = ROOT / "profiles" / "valu.json"
-            vi = json.loads(vf.read_text()).get(workload + "_standalone") if vf.exists() else None
+            vi, vi_src = stamped("valu.json", workload + "_standalone", build)
             if vi:
                 vst = {s: vi[s] / (stage_ms[s] * 1e-3) / 1e9 for s in vi if stage_ms.get(s, 0) > 0}
                 vdom = max(vst, key=lambda s: stage_ms[s])
                 out["valu_roofline"] = {
                     "bound": "valu", "unit": "G wave-instructions/s", "peak": VALU_PEAK_GIPS,
-                    "peak_def": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction",
+                    "peak_def": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction of the packed-16-bit / "
+                                "dot / perm / sad / shift / multiply class (profiles/r03/mulrate_r3b.log); the "
+                                f"add / logic / mov class issues at ~2.4 cycles ({VALU_PEAK_FAST_CLASS_GIPS:.0f} G/s)",
                     "kernel": STAGE_KERNELS[vdom], "achieved": round(vst[vdom], 2),
                     "frac": round(vst[vdom] / VALU_PEAK_GIPS, 4),
                     "stages": {s: {"inst_per_step": int(vi[s]), "achieved": round(v, 2),
                                    "frac": round(v / VALU_PEAK_GIPS, 4)} for s, v in vst.items()},
                     "pipeline_frac": (round(sum(vi.values()) * pairs_per_s / world / P / 1e9 / VALU_PEAK_GIPS, 4)
                                       if pairs_per_s else None),
-                    "source": "profiles/valu.json " + workload + "_standalone (rocprofv3 --pmc SQ_INSTS_VALU)"}
+                    "source": vi_src + " (rocprofv3 --pmc SQ_INSTS_VALU)"}
+            else:
+                out["valu_roofline"] = {"dropped": vi_src}
         if gather is not None:
             out["with_gather"] = gather
+        if c4 is not None:
+            out["c4_strong"] = c4
+        if hf is not None:
+            out["host_fed"] = hf
+        if c3 is not None:
+            out["c3_frame"] = {k: c3[k] for k in ("frames_per_s", "frames", "latency_ms", "parity", "workload",
+                                                  "speedup_vs_reference_frame", "what")}
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if world > 1:

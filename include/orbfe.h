@@ -72,6 +72,11 @@ const char* orbfe_last_error(void);
 /* library build string ("gfx950 ...") */
 const char* orbfe_version(void);
 
+/* Build identity: the first 16 hex digits of the SHA-256 of the sources and headers the library was built
+ * from (Makefile).  Measurement files (profiles/traffic.json, profiles/valu.json) record it, and bench.py
+ * uses their per-kernel figures only when it matches the loaded library. */
+const char* orbfe_build_id(void);
+
 /* GetLevels/GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
  * GetInverseScaleSigmaSquares (ORBextractor.h:62-82).  Each array has nlevels floats; any
  * pointer may be NULL.  n_per_level receives mnFeaturesPerLevel (ORBextractor.cpp:435-446). */
@@ -164,11 +169,6 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
  * each on an internal stream (fork from / join into the caller's stream); 1..4, default 4.  Results and
  * their layout do not depend on it. */
 int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
-
-/* orbfe_set_blur_fork: accepted and ignored (kept for ABI stability).  Round 1 ran a full-pyramid k_blur
- * that could fork onto a side stream; the blur is now fused into the descriptor kernel (k_orb), which
- * blurs only each keypoint's neighbourhood, so there is nothing to fork. */
-int orbfe_set_blur_fork(orbfe_handle h, int32_t on);
 
 /* Device result layout of the last batch (pointers into handle-owned device memory):
  *   kps   : n_images x cap  orbfe_keypoint   (cap = *kp_cap)
@@ -282,11 +282,11 @@ int orbfe_png_read_batch(const char* const* paths, int32_t n, int32_t width, int
 
 /* ---- live stage timing --------------------------------------------------------------------------
  * While profiling is on, every batch enqueued on the handle records HIP events around its stages:
- * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 blur (empty: fused into describe),
- * 4 describe (k_orb: IC angle + per-keypoint 7x7 blur + steered BRIEF), 5 stereo.
+ * 0 resize (all pyramid levels), 1 detect (FAST cells), 2 octree, 3 describe (k_orb: IC angle +
+ * per-keypoint 7x7 blur + steered BRIEF), 4 stereo (row buckets + k_stereo).
  * orbfe_profile_read synchronises and returns the summed milliseconds per stage (ms_per_stage holds
  * ORBFE_NSTAGES floats) over the recorded batches. */
-#define ORBFE_NSTAGES 6
+#define ORBFE_NSTAGES 5
 int orbfe_profile_begin(orbfe_handle h, int32_t max_batches);
 int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches);
 

@@ -48,6 +48,7 @@ SIGNATURES = {
     "orbfe_destroy": [C.c_void_p],
     "orbfe_last_error": [],
     "orbfe_version": [],
+    "orbfe_build_id": [],
     "orbfe_get_scales": [C.c_void_p] + [C.c_void_p] * 5,
     "orbfe_extract": [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
                       C.POINTER(C.c_int32)],
@@ -95,7 +96,6 @@ SIGNATURES = {
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
     "orbfe_set_lanes": [C.c_void_p, C.c_int32],
-    "orbfe_set_blur_fork": [C.c_void_p, C.c_int32],
     "orbfe_vocab_load_text": [C.c_char_p, C.POINTER(C.c_void_p)],
     "orbfe_vocab_create": [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_void_p, C.POINTER(C.c_void_p)],
@@ -132,7 +132,7 @@ def lib() -> C.CDLL:
             if fn is None:
                 raise OSError(f"{LIB_PATH} does not export {name}")
             fn.argtypes = argtypes
-            fn.restype = C.c_char_p if name in ("orbfe_last_error", "orbfe_version") else C.c_int
+            fn.restype = C.c_char_p if name in ("orbfe_last_error", "orbfe_version", "orbfe_build_id") else C.c_int
         _lib = L
     return _lib
 
@@ -159,6 +159,12 @@ def make_params(nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int
 
 def version() -> str:
     return lib().orbfe_version().decode()
+
+
+def build_id() -> str:
+    """SHA-256 prefix of the sources the loaded library was built from (orbfe_build_id)."""
+    fn = getattr(lib(), "orbfe_build_id", None)
+    return fn().decode() if fn is not None else "unknown"
 
 
 def gpu_available() -> bool:

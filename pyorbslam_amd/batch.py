@@ -21,7 +21,7 @@ KITTI_FX = 718.856   # KITTI00-02.yaml Camera.fx
 class StereoFrontEnd:
     def __init__(self, width: int = 1241, height: int = 376, max_pairs: int = 64, nfeatures: int = 2000,
                  scaleFactor: float = 1.2, nlevels: int = 8, iniThFAST: int = 20, minThFAST: int = 7,
-                 resize_simd_lanes: int = 16, lanes: int = 4, blur_fork: bool = False):
+                 resize_simd_lanes: int = 16, lanes: int = 4):
         self.width, self.height, self.max_pairs = int(width), int(height), int(max_pairs)
         self._params = _lib.make_params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes)
         h = C.c_void_p()
@@ -30,7 +30,6 @@ class StereoFrontEnd:
         call("orbfe_batch_reserve", h, self.width, self.height, 2 * self.max_pairs)
         # concurrent chunks of enqueue() on internal streams (results are independent of it)
         call("orbfe_set_lanes", h, int(lanes))
-        call("orbfe_set_blur_fork", h, int(bool(blur_fork)))  # no-op since the blur moved into k_orb
         v = BatchView()
         call("orbfe_batch_view_get", h, C.byref(v))
         self.kp_cap = v.kp_cap

@@ -67,6 +67,9 @@ struct ResizeY {
     int16_t b0, b1;
 };
 
+// Kernels of the pipeline, indexing Geo::prio.
+enum { kPrioResize = 0, kPrioDetect, kPrioOctree, kPrioOrb, kPrioBucket, kPrioStereo, kPrioN };
+
 // Per-geometry constants passed by value to every kernel.
 struct Geo {
     int nlevels;
@@ -91,6 +94,7 @@ struct Geo {
     int fd_mp;           // k_detect: u8 M map pitch in bytes (>= widest window + 6, multiple of 16)
     int fd_pq;           // k_detect: pair-queue entries (>= ceil(ww/2) * wh)
     int fd_alt;          // k_detect: largest cell slot_cap (minTh survivors staged in the ROI area)
+    int prio[8];         // wave issue priority (s_setprio) per kernel, kPrio* below; 0 = default (ORBFE_PRIO)
     int umax[16];
     float scale[kMaxLevels];
     float inv_scale[kMaxLevels];

@@ -38,11 +38,9 @@ inline short sat_short(int v) { return (short)std::min(std::max(v, -32768), 3276
 
 // concurrent chunks of orbfe_frontend_batch_device (the box exposes 4 hardware queues per process)
 constexpr int kLanes = 4;
-// profiling events per batch and the event pair of each stage (resize, detect, octree, blur, describe,
-// stereo); see prof_mark
-constexpr int kProfEvents = 9;
-constexpr int kProfFrom[ORBFE_NSTAGES] = {0, 1, 2, 7, 4, 5};
-constexpr int kProfTo[ORBFE_NSTAGES] = {1, 2, 3, 8, 5, 6};
+// profiling events per batch: stage k (resize, detect, octree, describe, stereo) spans events k -> k + 1;
+// see prof_mark
+constexpr int kProfEvents = ORBFE_NSTAGES + 1;
 
 struct orbfe_ctx {
     orbfe_params prm{};
@@ -101,6 +99,8 @@ struct orbfe_ctx {
     hipEvent_t lane_done[kLanes] = {};
     hipEvent_t lane_fork = nullptr;
     hipStream_t last_stream = nullptr;
+    hipEvent_t batch_done = nullptr;   // recorded on last_stream at the end of every batch enqueue
+    bool batch_done_rec = false;
     const uint8_t* last_in = nullptr;  // device input of the last extraction
     int64_t last_pitch = 0;
     int last_images = 0, last_pairs = 0;
@@ -126,6 +126,7 @@ struct orbfe_ctx {
             if (lane_done[k]) (void)hipEventDestroy(lane_done[k]);
         }
         if (lane_fork) (void)hipEventDestroy(lane_fork);
+        if (batch_done) (void)hipEventDestroy(batch_done);
     }
 };
 
@@ -363,6 +364,13 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
     // candidates in LDS when the node arrays leave room for them, else they stay in the global scratch
     // (very large per-level feature counts, e.g. one level with thousands of features)
+    // ORBFE_PRIO=r,d,o,k,b,s: s_setprio level (0..3) of resize, detect, octree, k_orb, stereo bucket,
+    // k_stereo (tuning knob for the 4-stream step; default all 0)
+    if (const char* e = std::getenv("ORBFE_PRIO")) {
+        int k = 0;
+        for (const char* q = e; *q && k < kPrioN; ++q)
+            if (*q >= '0' && *q <= '3') g.prio[k++] = *q - '0';
+    }
     g.oct_keys = kOctKeys;
     if (const char* e = std::getenv("ORBFE_OCT_KEYS")) g.oct_keys = std::max(0, std::min(kOctKeys, std::atoi(e)));
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_keys = 0;
@@ -419,9 +427,19 @@ std::vector<uint32_t> orb_tables(const int* umax) {
     return t;
 }
 
+// Every call that enqueues work on (or reallocates) the handle's device buffers ends the validity of the
+// results an earlier orbfe_extract / orbfe_frame_extract left there: the getters of those results then
+// fail with ORBFE_ESTATE instead of reading buffers, offsets and a geometry that no longer belong together.
+void invalidate_results(orbfe_ctx& c) {
+    c.have_single = false;
+    c.have_frame = false;
+    c.frame_pyr = false;
+}
+
 void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     if (W <= 0 || H <= 0 || max_images <= 0) throw Error(ORBFE_EINVAL, "bad reserve geometry");
     if (W != c.W || H != c.H) {
+        invalidate_results(c);
         build_geometry(c, W, H);
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
@@ -437,9 +455,9 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.d_yt.ensure(c.yt.size());
         if (!c.yt.empty())
             HIPCK(hipMemcpy(c.d_yt.p, c.yt.data(), c.yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
-        c.have_single = false;
     }
     if (max_images > c.max_images) {
+        invalidate_results(c);  // the per-image buffers may move
         const Geo& g = c.geo;
         const size_t n = (size_t)max_images;
         c.d_ws.ensure(n * g.ws_bytes);
@@ -467,10 +485,8 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     }
 }
 
-// record event `k` of the current profiled batch.  Launch stream: 0 start, 1 after resize, 2 after
-// detect, 3 after octree, 4 describe (k_orb) starts, 5 after describe, 6 after stereo; 7 / 8 bracket the
-// blur stage, which is empty since the blur was fused into k_orb (kept so the stage list of the ABI stays
-// stable).  Stage k spans events kProfFrom[k] -> kProfTo[k].
+// record event `k` of the current profiled batch on the launch stream: 0 start, 1 after resize, 2 after
+// detect, 3 after octree, 4 after describe (k_orb), 5 after stereo.
 void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
     if (!c.prof_on || c.prof_n >= c.prof_max) return;
     HIPCK(hipEventRecord(c.prof_ev[(size_t)c.prof_n * kProfEvents + k], s));
@@ -501,12 +517,8 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
                         s));
     if (prof) prof_mark(c, s, 3);
-    // the blur is fused into k_orb (each keypoint blurs its own neighbourhood): the blur stage is empty
-    if (prof) prof_mark(c, s, 7);
-    if (prof) prof_mark(c, s, 8);
-    if (prof) prof_mark(c, s, 4);
     HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
-    if (prof) prof_mark(c, s, 5);
+    if (prof) prof_mark(c, s, 4);
 }
 
 void check_extract(orbfe_ctx& c, int64_t pitch, int n) {
@@ -571,15 +583,24 @@ void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int 
     HIPCK(launch_stereo(g, a, n, s));
 }
 
+// Marks the end of a batch enqueue on s: orbfe_batch_pack_device orders its k_pack after it, whatever
+// stream the caller packs on.
+void record_batch_done(orbfe_ctx& c, hipStream_t s) {
+    if (!c.batch_done) HIPCK(hipEventCreateWithFlags(&c.batch_done, hipEventDisableTiming));
+    HIPCK(hipEventRecord(c.batch_done, s));
+    c.batch_done_rec = true;
+}
+
 void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStream_t s) {
     if (n_pairs <= 0) return;
     if (2 * n_pairs > c.last_images) throw Error(ORBFE_ESTATE, "stereo batch needs 2*n_pairs extracted images");
     stereo_range(c, c.last_in, c.last_pitch, 0, n_pairs, bf, fx, s);
     c.last_bf = bf;
     c.last_fx = fx;
-    prof_mark(c, s, 6);
+    prof_mark(c, s, 5);
     if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
     c.last_pairs = n_pairs;
+    record_batch_done(c, s);
 }
 
 // The whole front-end for n_pairs pairs as up to kLanes concurrent chunks, each on its own internal
@@ -594,7 +615,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     if (K == 1) {
         extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true);
         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
-        prof_mark(c, s, 6);
+        prof_mark(c, s, 5);
     } else {
         if (!c.lane_stream[0]) {
             for (int k = 0; k < kLanes; ++k) {
@@ -610,7 +631,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
             extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k);
             stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
-            if (k == 0) prof_mark(c, ls, 6);
+            if (k == 0) prof_mark(c, ls, 5);
             HIPCK(hipEventRecord(c.lane_done[k], ls));
         }
         for (int k = 0; k < K; ++k) HIPCK(hipStreamWaitEvent(s, c.lane_done[k], 0));
@@ -623,6 +644,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     c.last_stream = s;
     c.last_bf = bf;
     c.last_fx = fx;
+    record_batch_done(c, s);
 }
 
 hipStream_t own(orbfe_ctx& c) {
@@ -706,7 +728,7 @@ int orbfe_extract(orbfe_handle h, const uint8_t* img, int32_t width, int32_t hei
     return guarded([&] {
         if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");
         *n_out = 0;
-        h->have_single = false;
+        invalidate_results(*h);
         if (width <= 0 || height <= 0) return;  // _image.empty() -> return (ORBextractor.cpp:1045-1046)
         if (!img || stride < width) throw Error(ORBFE_EINVAL, "bad image pointer / stride");
         reserve(*h, width, height, std::max(h->max_images, 1));
@@ -757,8 +779,7 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
                         int32_t stride, double bf, float fx, int32_t want_pyramid) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
-        h->have_frame = h->frame_pyr = false;
-        h->have_single = false;
+        invalidate_results(*h);
         const bool empty = width <= 0 || height <= 0;  // operator_kd: _image.empty() -> return (:1045-1046)
         if (!empty) {
             if (!left || !right || stride < width) throw Error(ORBFE_EINVAL, "bad image pointer / stride");
@@ -946,7 +967,7 @@ int orbfe_extract_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t 
     return guarded([&] {
         if (!h || !d_images) throw Error(ORBFE_EINVAL, "null argument");
         if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
-        h->have_single = false;
+        invalidate_results(*h);
         enqueue_extract(*h, d_images, img_pitch, n_images, (hipStream_t)hip_stream);
     });
 }
@@ -954,6 +975,7 @@ int orbfe_extract_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t 
 int orbfe_stereo_batch_device(orbfe_handle h, int32_t n_pairs, double bf, float fx, void* hip_stream) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        invalidate_results(*h);  // overwrites the stereo buffers and the row buckets
         enqueue_stereo_batch(*h, n_pairs, bf, fx, (hipStream_t)hip_stream);
     });
 }
@@ -963,7 +985,7 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
     return guarded([&] {
         if (!h || !d_images) throw Error(ORBFE_EINVAL, "null argument");
         if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
-        h->have_single = false;
+        invalidate_results(*h);
         enqueue_frontend(*h, d_images, img_pitch, n_pairs, bf, fx, (hipStream_t)hip_stream);
     });
 }
@@ -973,13 +995,6 @@ int orbfe_set_lanes(orbfe_handle h, int32_t lanes) {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
         if (lanes < 1 || lanes > kLanes) throw Error(ORBFE_EINVAL, "lanes must be 1..4");
         h->lanes = lanes;
-    });
-}
-
-int orbfe_set_blur_fork(orbfe_handle h, int32_t on) {
-    return guarded([&] {
-        if (!h) throw Error(ORBFE_EINVAL, "null handle");
-        (void)on;  // accepted for ABI stability: the blur is fused into k_orb, there is no blur stage to fork
     });
 }
 
@@ -1034,6 +1049,8 @@ int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_byte
         if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
         PackArgs a{h->d_count.p, h->d_kps.p, h->d_desc.p, h->d_uR.p, h->d_depth.p, h->d_status.p, h->geo.kp_cap,
                    rec_bytes};
+        // the records are read after the batch that produced them, on whichever stream the caller packs
+        if (h->batch_done_rec) HIPCK(hipStreamWaitEvent((hipStream_t)hip_stream, h->batch_done, 0));
         HIPCK(launch_pack(a, d_records, pair0, n_pairs, (hipStream_t)hip_stream));
     });
 }
@@ -1307,11 +1324,10 @@ int orbfe_profile_read(orbfe_handle h, float* ms_per_stage, int32_t* n_batches) 
         for (int k = 0; k < ORBFE_NSTAGES; ++k) ms_per_stage[k] = 0.f;
         for (int b = 0; b < h->prof_n; ++b) {
             hipEvent_t* e = &h->prof_ev[(size_t)b * kProfEvents];
-            HIPCK(hipEventSynchronize(e[6]));
-            HIPCK(hipEventSynchronize(e[8]));
+            HIPCK(hipEventSynchronize(e[ORBFE_NSTAGES]));
             for (int k = 0; k < ORBFE_NSTAGES; ++k) {
                 float ms = 0.f;
-                HIPCK(hipEventElapsedTime(&ms, e[kProfFrom[k]], e[kProfTo[k]]));
+                HIPCK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
                 ms_per_stage[k] += ms;
             }
         }

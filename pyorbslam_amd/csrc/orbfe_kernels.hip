@@ -71,6 +71,17 @@ __device__ __forceinline__ int wave_sum(int v) {
            __builtin_amdgcn_readlane(v, 48);
 }
 
+// Wave issue priority of a kernel (Geo::prio, ORBFE_PRIO): raises a latency-bound stage above the
+// issue-bound waves of the other handles' stages sharing its SIMD (VALU issue goes by priority, then age).
+__device__ __forceinline__ void set_prio(const Geo& g, int k) {
+    switch (g.prio[k]) {
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
+}
+
 __device__ __forceinline__ int reflect101(int p, int n) {
     // one reflection suffices: every caller overshoots by less than n
     p = p < 0 ? -p : p;
@@ -184,6 +195,7 @@ template <int V>  // V: 0 full kernel; ablations for tools/microbench.py: 1 stag
 __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                 uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
+    set_prio(g, kPrioResize);
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     const LevelGeo& L = g.lv[l];
     uint4* s_sel = (uint4*)rs_lds;                       // L.rs_ngrp groups each
@@ -399,6 +411,7 @@ template <int V, int RP, int NS>
 __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
+    set_prio(g, kPrioDetect);
     constexpr int S = RP / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // ROI (max_rh rows x RP u16); after the M stage the same bytes stage the minTh survivors (u32 records)
@@ -715,6 +728,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                                                 uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
                                                 int* __restrict__ overflow, int maxcell, int stop,
                                                 long long* __restrict__ prof) {
+    set_prio(g, kPrioOctree);
     // stop (tools/microbench.py ablations): 1 after the candidate gather, 2 after the initial columns,
     // 3 after the full-division phase, 16 + l only level l, 64 + 8 l + n only level l and stop before
     // pass n; 0 = the whole algorithm
@@ -1241,6 +1255,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                                                     const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                     const uint32_t* __restrict__ tab) {
+    set_prio(g, kPrioOrb);
     __shared__ float4 s_pat[256];
     __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: (byte mask, m10 byte weights)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
@@ -1564,6 +1579,7 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
 // Also writes the compact (x, octave) record of every right keypoint.
 __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
+    set_prio(g, kPrioBucket);
     extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
     __shared__ int scan_tmp[257];
     const int pr = blockIdx.x, t = threadIdx.x;
@@ -1691,6 +1707,7 @@ __device__ __forceinline__ void sheared_words(const uint8_t* lvl, int stride, in
 }
 
 __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
+    set_prio(g, kPrioStereo);
     __shared__ int sad[16][11];
     // the 11 x 11 left and 11 x 21 right windows as u16 pixel + 512: left columns (2k, 2k + 1) per dword,
     // right columns (2k, 2k + 1) and (2k + 1, 2k + 2) per dword (both alignments of a shift's window)

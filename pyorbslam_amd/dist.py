@@ -107,28 +107,34 @@ def gather_results(records: np.ndarray, n_pairs_total: int, device=None, dst: in
     return np.concatenate([full[r, :shard(n_pairs_total, world, r)[1]] for r in range(world)], axis=0)
 
 
-def pack_device(frontends, pairs_per_handle: int, out) -> None:
-    """Pack every pair of the handles' last stereo batches into `out` ((handles * pairs, record_bytes) uint8
-    device tensor) with k_pack, on the current stream (orbfe_batch_pack_device)."""
+def pack_device(frontends, counts, out) -> None:
+    """Pack every pair of the handles' last stereo batches into `out` ((sum(counts), record_bytes) uint8 device
+    tensor, handle-major) with k_pack on the current stream; orbfe_batch_pack_device orders each pack after
+    the batch that produced its results, whatever stream that batch ran on."""
     import ctypes as C
     import torch
     from ._lib import call
     rb = out.shape[1]
     st = torch.cuda.current_stream(out.device).cuda_stream
-    for i, f in enumerate(frontends):
-        call("orbfe_batch_pack_device", f.handle, C.c_void_p(out[i * pairs_per_handle].data_ptr()), rb, 0,
-             pairs_per_handle, C.c_void_p(st))
+    o = 0
+    for f, n in zip(frontends, counts):
+        if n:
+            call("orbfe_batch_pack_device", f.handle, C.c_void_p(out[o].data_ptr()), rb, 0, n, C.c_void_p(st))
+        o += n
 
 
-def timed_gather(frontends, pairs_per_handle: int, device, world: int, rank: int, reps: int = 3) -> dict:
+def timed_gather(frontends, counts, device, world: int, rank: int, max_local: int | None = None,
+                 reps: int = 3) -> dict:
     """Pack (k_pack) + gather to rank 0 of every pair's results, timed like the bench step (barrier +
-    synchronise on both sides, max over ranks); the records of rank 0's own first pair are checked
-    against orbfe_batch_fetch."""
+    synchronise on both sides, max over ranks); every rank sends max_local records (its own pairs, padded:
+    uneven shards of a strong-scaling run).  The records of rank 0's own first pair are checked against
+    orbfe_batch_fetch."""
     import torch
     import torch.distributed as dist
-    n_local = len(frontends) * pairs_per_handle
+    n_local = int(sum(counts))
+    max_local = n_local if max_local is None else int(max_local)
     rb = record_bytes(frontends[0].kp_cap)
-    buf = torch.empty((n_local, rb), dtype=torch.uint8, device=device)
+    buf = torch.zeros((max_local, rb), dtype=torch.uint8, device=device)
     times = []
     full = None
     for _ in range(reps + 1):
@@ -136,7 +142,7 @@ def timed_gather(frontends, pairs_per_handle: int, device, world: int, rank: int
             dist.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        pack_device(frontends, pairs_per_handle, buf)
+        pack_device(frontends, counts, buf)
         # RCCL gathers the device buffer in place; a gloo rehearsal (several ranks on one GPU) stages it
         full = gather_records(buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu(), 0)
         torch.cuda.synchronize(device)
@@ -157,7 +163,8 @@ def timed_gather(frontends, pairs_per_handle: int, device, world: int, rank: int
               and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["status"], s["status"]))
         if not ok:
             raise RuntimeError("gathered record of pair 0 differs from orbfe_batch_fetch")
-    return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "pairs_gathered": world * n_local,
-            "bytes_to_rank0": world * n_local * rb, "record_check": ok,
+    return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "pairs_gathered": world * max_local,
+            "bytes_to_rank0": world * max_local * rb, "record_check": ok,
+            "GBs_into_rank0": round(world * max_local * rb / dt / 1e9, 2),
             "what": "k_pack on every rank + one gather of the records to rank 0 (RCCL with nccl, gloo on CPU), "
                     f"mean of {reps} after 1 warm-up, barrier + synchronize around each, max over ranks"}

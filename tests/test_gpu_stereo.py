@@ -239,7 +239,7 @@ def test_device_pack_records_match_fetch():
     torch.cuda.synchronize()
     rb = D.record_bytes(fes[0].kp_cap)
     buf = torch.zeros((6, rb), dtype=torch.uint8, device="cuda")
-    D.pack_device(fes, 3, buf)
+    D.pack_device(fes, [3, 3], buf)
     torch.cuda.synchronize()
     host = buf.cpu().numpy()
     for i, f in enumerate(fes):
@@ -293,20 +293,95 @@ def test_undistort_keypoints_drop_in():
 
 
 def test_default_bench_configuration_sampled():
-    """The exact default bench step (512 KITTI pairs as 4 handles x 128 pairs on 4 streams, lanes 1) and the
-    bench's own parity check: every handle's overflow word, its first and last pair bit for bit against the
-    oracle extractor and the stereo restatement."""
+    """The exact default bench step (bench.Shard: 512 KITTI pairs as 4 handles x 128 pairs on 4 streams, lanes
+    1) and the bench's own parity check: every handle's overflow word, its first and last pair bit for bit
+    against the oracle extractor and the stereo restatement."""
     torch = pytest.importorskip("torch")
     import bench
-    from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
     P, S = 512, 4
     host = synth.make_batch(P, seed0=0)
     images = torch.from_numpy(host).cuda()
-    fes = [StereoFrontEnd(max_pairs=P // S, lanes=1) for _ in range(S)]
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
+    sh = bench.Shard(images, P, S, torch.device("cuda", 0), 1241, 376, 2000)
+    assert sh.counts == [128] * 4
     for _ in range(2):  # the bench repeats the step on the same buffers
-        for i, (f, st) in enumerate(zip(fes, streams)):
-            f.enqueue(images[2 * (P // S) * i:2 * (P // S) * (i + 1)], P // S, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
+        sh.step()
     torch.cuda.synchronize()
-    checked, ovf, bad = bench.parity_check(fes, host, P // S, 1241, 376, 2000)
+    checked, ovf, bad = bench.parity_check(sh.fes, sh.counts, host, 1241, 376, 2000)
     assert ovf == 0 and not bad and checked == 8, bad
+
+
+def test_c4_shards_and_host_fed():
+    """C4's shards (64 pairs over 1, 2, 4 or 8 ranks: 64, 32, 16, 8 pairs, up to 4 handles each), uneven
+    handle splits, and the host-fed pass (pinned H2D + compute + packed records D2H, double-buffered) whose
+    records must equal the handles' own results; parity of the uneven shard against the oracle."""
+    torch = pytest.importorskip("torch")
+    import bench
+    dev = torch.device("cuda", 0)
+    for world in (1, 2, 4, 8):
+        assert sum(bench.shard(64, world, r)[1] for r in range(world)) == 64
+    host = synth.make_batch(7, seed0=300)
+    images = torch.from_numpy(host).to(dev)
+    sh = bench.Shard(images, 7, 4, dev, 1241, 376, 2000)
+    assert sh.counts == [2, 2, 2, 1]
+    sh.step()
+    torch.cuda.synchronize()
+    checked, ovf, bad = bench.parity_check(sh.fes, sh.counts, host, 1241, 376, 2000)
+    assert ovf == 0 and not bad and checked == 7, bad
+    hf = bench.host_fed(sh, host, dev, 1, 3, 1)
+    assert hf["record_check"] and hf["value"] > 0
+
+
+def test_pack_orders_after_batch_on_another_stream():
+    """orbfe_batch_pack_device on a stream other than the batch's waits for that batch: pack right
+    after enqueue, without a host synchronisation in between."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd import dist as D
+    from pyorbslam_amd.batch import StereoFrontEnd
+    imgs = torch.from_numpy(synth.make_batch(4, seed0=90)).cuda()
+    f = StereoFrontEnd(max_pairs=4, lanes=1)
+    side, other = torch.cuda.Stream(), torch.cuda.Stream()
+    rb = D.record_bytes(f.kp_cap)
+    buf = torch.zeros((4, rb), dtype=torch.uint8, device="cuda")
+    f.enqueue(imgs, 4, stream_ptr=side.cuda_stream)
+    with torch.cuda.stream(other):
+        D.pack_device([f], [4], buf)
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    for p in range(4):
+        u = D.unpack(f.kp_cap, host[p])
+        kl, dl = f.fetch_image(2 * p)
+        assert u["kps_left"].tobytes() == kl.tobytes() and np.array_equal(u["desc_left"], dl), p
+
+
+def test_frame_results_invalidated_by_other_work():
+    """after orbfe_frame_extract, a reservation of another size or a batch extraction on the same
+    handle ends the frame's results; the frame getters then fail with ESTATE instead of reading stale offsets."""
+    import ctypes as C
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd import _lib
+    from pyorbslam_amd._lib import call
+    from pyorbslam_amd.batch import StereoFrontEnd
+    L, R = synth.make_pair(11)
+    fe = StereoFrontEnd(max_pairs=1, lanes=1)
+    h = fe.handle
+    call("orbfe_frame_extract", h, _lib.ptr(L), _lib.ptr(R), 1241, 376, 1241, BF, float(np.float32(FX)), 0)
+    n = C.c_int32()
+    kps = np.empty(fe.kp_cap, _lib.KP_DTYPE)
+    desc = np.empty((fe.kp_cap, 32), np.uint8)
+    call("orbfe_frame_fetch", h, 0, _lib.ptr(kps), _lib.ptr(desc), fe.kp_cap, C.byref(n))  # valid
+    assert n.value > 0
+    call("orbfe_batch_reserve", h, 641, 333, 2)
+    out = np.zeros(1241 * 376, np.uint8)
+    w, hh = C.c_int32(), C.c_int32()
+    for fn, args in (("orbfe_frame_pyramid", (h, 0, 0, _lib.ptr(out), C.byref(w), C.byref(hh))),
+                     ("orbfe_frame_fetch", (h, 0, _lib.ptr(kps), _lib.ptr(desc), fe.kp_cap, C.byref(n)))):
+        with pytest.raises(_lib.OrbfeError) as e:
+            call(fn, *args)
+        assert e.value.code == -5, fn
+    call("orbfe_batch_reserve", h, 1241, 376, 2)
+    call("orbfe_frame_extract", h, _lib.ptr(L), _lib.ptr(R), 1241, 376, 1241, BF, float(np.float32(FX)), 0)
+    imgs = torch.from_numpy(synth.make_batch(1, seed0=12)).cuda()
+    fe.enqueue(imgs, 1)
+    with pytest.raises(_lib.OrbfeError) as e:
+        call("orbfe_frame_pyramid", h, 1, 2, _lib.ptr(out), C.byref(w), C.byref(hh))
+    assert e.value.code == -5

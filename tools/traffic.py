@@ -9,9 +9,26 @@ import csv
 import glob
 import json
 import sys
+from pathlib import Path
 
 STAGES = {"resize": ["k_resize"], "detect": ["k_detect"], "octree": ["k_octree"],
-          "blur": ["k_blur"], "describe": ["k_orb", "k_describe"], "stereo": ["k_stereo_bucket", "k_stereo"]}
+          "describe": ["k_orb"], "stereo": ["k_stereo_bucket", "k_stereo"]}
+
+
+def stamp() -> dict:
+    """Build id of the library the PMC runs measured (the in-tree build that travelled to the GPU box) and
+    the git revision: bench.py uses an entry only when the build id matches the library it loads."""
+    import subprocess
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from pyorbslam_amd import _lib
+    try:
+        rev = subprocess.check_output(["git", "rev-parse", "--short=12", "HEAD"], cwd=Path(__file__).resolve().parents[1],
+                                      text=True).strip()
+        dirty = subprocess.call(["git", "diff", "--quiet", "HEAD", "--", "pyorbslam_amd/csrc", "include"],
+                                cwd=Path(__file__).resolve().parents[1]) != 0
+    except Exception:
+        rev, dirty = "unknown", False
+    return {"build_id": _lib.build_id(), "git_rev": rev + ("+uncommitted-kernel-edits" if dirty else "")}
 
 
 def per_kernel(d, counter):
@@ -45,6 +62,7 @@ def main():
         pass
     data[workload] = {st: v["bytes"] for st, v in res.items()}
     data[workload + "_detail"] = res
+    data[workload + "_meta"] = stamp()
     json.dump(data, open(out, "w"), indent=1, sort_keys=True)
     for st, v in res.items():
         print(f"{st:9s} fetch(raw) {v['fetch_raw_bytes'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB  "

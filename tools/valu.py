@@ -9,7 +9,7 @@ import glob
 import json
 import sys
 
-from traffic import STAGES
+from traffic import STAGES, stamp
 
 
 def per_kernel(d, counter):
@@ -40,6 +40,7 @@ def main():
         pass
     data[workload] = {st: v["valu_inst"] for st, v in res.items()}
     data[workload + "_detail"] = res
+    data[workload + "_meta"] = stamp()
     json.dump(data, open(out, "w"), indent=1, sort_keys=True)
     for st, v in res.items():
         print(f"{st:9s} VALU {v['valu_inst'] / 1e6:9.1f} M  LDS {v['lds_inst'] / 1e6:8.1f} M wave-instructions per step")
