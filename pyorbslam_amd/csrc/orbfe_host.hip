@@ -93,6 +93,10 @@ struct orbfe_ctx {
     bool prof_on = false;
 
     hipStream_t own_stream = nullptr;
+    // ORBFE_STAGE_REPEAT=r,d,o,k,s (development aid): launches of each stage per batch (default 1 each).
+    // Every stage is idempotent, so a second launch measures the stage's marginal cost inside the
+    // concurrent multi-handle step, where its standalone time says little.
+    int stage_rep[ORBFE_NSTAGES] = {1, 1, 1, 1, 1};
     // orbfe_frontend_batch_device: up to kLanes concurrent chunks of the batch on internal streams
     int lanes = kLanes;  // orbfe_set_lanes
     hipStream_t lane_stream[kLanes] = {};
@@ -509,15 +513,19 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     uint8_t* desc = c.d_desc.p + (int64_t)i0 * g.kp_cap * 32;
     int* count = c.d_count.p + i0;
     if (prof) prof_mark(c, s, 0);
-    for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
+    for (int r = 0; r < c.stage_rep[0]; ++r)
+        for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
     if (prof) prof_mark(c, s, 1);
     (void)lane;
-    if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
+    for (int r = 0; r < c.stage_rep[1]; ++r)
+        if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
     if (prof) prof_mark(c, s, 2);
-    HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
-                        s));
+    for (int r = 0; r < c.stage_rep[2]; ++r)
+        HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
+                            s));
     if (prof) prof_mark(c, s, 3);
-    HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
+    for (int r = 0; r < c.stage_rep[3]; ++r)
+        HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
     if (prof) prof_mark(c, s, 4);
 }
 
@@ -580,7 +588,7 @@ void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int 
     a.out_stride = g.kp_cap;
     stereo_buffers(c, a, p0);
     stereo_consts(bf, fx, a);
-    HIPCK(launch_stereo(g, a, n, s));
+    for (int r = 0; r < c.stage_rep[4]; ++r) HIPCK(launch_stereo(g, a, n, s));
 }
 
 // Marks the end of a batch enqueue on s: orbfe_batch_pack_device orders its k_pack after it, whatever
@@ -690,6 +698,11 @@ int orbfe_create(const orbfe_params* params, orbfe_handle* out) {
         if (!params || !out) throw Error(ORBFE_EINVAL, "null argument");
         std::unique_ptr<orbfe_ctx> c(new orbfe_ctx());
         c->prm = *params;
+        if (const char* e = std::getenv("ORBFE_STAGE_REPEAT")) {
+            int k = 0;
+            for (const char* q = e; *q && k < ORBFE_NSTAGES; ++q)
+                if (*q >= '0' && *q <= '9') c->stage_rep[k++] = *q - '0';
+        }
         build_tables(*c);
         *out = c.release();
     });

@@ -120,10 +120,14 @@ void decode(const uint8_t* data, size_t size, uint8_t* out, int64_t stride, int*
         } else if (bpp == 2) {
             for (int x = 0; x < info.w; ++x) o[x] = cur[2 * x];
         } else {
-            // libpng png_do_rgb_to_gray, 8-bit, no gamma: (rc R + gc G + bc B + 16384) >> 15
+            // OpenCV's PNG decoder asks libpng for png_set_rgb_to_gray(png, 1, 0.299, 0.587):
+            // png_set_rgb_to_gray_fixed truncates the coefficients to 15 bits (rc = 29900 * 32768 / 100000
+            // = 9797, gc = 19234, bc = 32768 - rc - gc = 3737) and png_do_rgb_to_gray's 8-bit no-gamma path
+            // truncates the sum ((rc R + gc G + bc B) >> 15; grey pixels pass unchanged, which the formula
+            // also gives).  Parity unpinned: no colour fixture exists in the reference.
             for (int x = 0; x < info.w; ++x) {
                 const uint8_t* p = &cur[(size_t)x * bpp];
-                o[x] = (uint8_t)((9798u * p[0] + 19235u * p[1] + 3735u * p[2] + 16384u) >> 15);
+                o[x] = (uint8_t)((9797u * p[0] + 19234u * p[1] + 3737u * p[2]) >> 15);
             }
         }
         std::swap(prev, cur);

@@ -216,20 +216,25 @@ def features_in_areas(frame, queries) -> list:
 _uright_cache = weakref.WeakKeyDictionary()
 
 
-def _u_right(frame):
+def _u_right(frame, with_kinds: bool = False):
+    """frame.mvuRight widened to a float64 array (cached while the list is the same object); with_kinds
+    also returns whether every entry is already a double (Python float / int or np.float64), i.e. whether
+    `python_float - mvuRight[i]` evaluates in double under NumPy 2's promotion rules (NEP 50: a Python
+    float meeting an np.float32 stays float32)."""
     vals = frame.mvuRight
     try:
         ent = _uright_cache.get(frame)
     except TypeError:
         ent = None
-    if ent is not None and ent[0] == (id(vals), len(vals)):
-        return ent[1]
-    arr = np.fromiter((float(v) for v in vals), np.float64, count=len(vals))
-    try:
-        _uright_cache[frame] = ((id(vals), len(vals)), arr)
-    except TypeError:
-        pass
-    return arr
+    if ent is None or ent[0] != (id(vals), len(vals)):
+        arr = np.fromiter((float(v) for v in vals), np.float64, count=len(vals))
+        all_double = all(type(v) in (float, int, np.float64) for v in vals)
+        ent = ((id(vals), len(vals)), arr, all_double)
+        try:
+            _uright_cache[frame] = ent
+        except TypeError:
+            pass
+    return (ent[1], ent[2]) if with_kinds else ent[1]
 
 
 def _blocked(frame):
@@ -463,7 +468,11 @@ class ORBMatcher:
         if not all(_is_f64(x) for x in xr_all):
             return None
         n_frame = len(frame.mvpMapPoints)
-        u_right = _u_right(frame)
+        u_right, u_double = _u_right(frame, with_kinds=True)
+        # ORBMatcher.py's er = abs(XR - mvuRight[idx]): a Python-float XR against an np.float32 entry
+        # evaluates in float32 (NEP 50), which the double selection in C does not reproduce
+        if not u_double and any(type(x) is float for x in xr_all):
+            return None
         if len(u_right) != n_frame or len(grid[4]) != n_frame:
             return None
         n = len(queries)

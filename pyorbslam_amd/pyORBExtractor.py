@@ -35,9 +35,14 @@ class ORBextractor:
         self._kps = np.zeros(0, KP_DTYPE)
         self._desc = np.zeros((0, 32), np.uint8)
         self._extracted = False
-        # after operator_kd_stereo: (handle, side) whose frame holds this extractor's pyramid, the stereo
-        # result of the pair (left extractor), and the right image whose results wait for ExtractORB(1)
+        # after operator_kd_stereo: (left extractor, side) whose frame holds this extractor's pyramid, the
+        # stereo result of the pair (left extractor), and the right image whose results wait for
+        # ExtractORB(1).  The left extractor lists the extractors reading its frame (_dependents) and hands
+        # them a host copy of their pyramid (_pyr_cache) before its next extraction replaces the frame, so
+        # every extractor's pyramid stays its own, as in the reference.
         self._pyr_src = None
+        self._pyr_cache = None
+        self._dependents = []
         self.stereo_result = None
         self._pending_image = None
 
@@ -78,14 +83,18 @@ class ORBextractor:
         (opencv_type_casters.h:232-239 ignores Mat::step); sheared=False gives the true levels."""
         if not self._extracted:
             return [np.zeros((0, 0), np.uint8) for _ in range(self._nlevels)]
+        if self._pyr_cache is not None:
+            if not sheared:
+                raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
+            return [a.copy() for a in self._pyr_cache]
         out = []
         for l in range(self._nlevels):
             w, h = C.c_int32(), C.c_int32()
             if self._pyr_src is not None and sheared:
-                src, side = self._pyr_src
-                call("orbfe_frame_pyramid", src, side, l, None, C.byref(w), C.byref(h))
+                owner, side = self._pyr_src
+                call("orbfe_frame_pyramid", owner.handle, side, l, None, C.byref(w), C.byref(h))
                 a = np.empty((h.value, w.value), np.uint8)
-                call("orbfe_frame_pyramid", src, side, l, ptr(a), C.byref(w), C.byref(h))
+                call("orbfe_frame_pyramid", owner.handle, side, l, ptr(a), C.byref(w), C.byref(h))
             else:
                 if self._pyr_src is not None:
                     raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
@@ -111,6 +120,15 @@ class ORBextractor:
         else:
             self._kps, self._desc = kps[:n].copy(), desc[:n].copy()
 
+    def _release_frame(self) -> None:
+        """Before this handle's frame is replaced: the extractors still reading their pyramid from it get a
+        host copy of it (the right extractor of an earlier pair must keep its own pyramid)."""
+        for ex in self._dependents:
+            if ex._pyr_src is not None and ex._pyr_src[0] is self:
+                ex._pyr_cache = ex.GetImagePyramid() if ex._extracted else None
+                ex._pyr_src = None
+        self._dependents = []
+
     def extract(self, image) -> tuple[np.ndarray, np.ndarray]:
         """operator_kd with structured-array output (no per-keypoint Python objects)."""
         img = as_gray_u8(image)
@@ -119,7 +137,9 @@ class ORBextractor:
         kps = np.empty(cap, KP_DTYPE)
         desc = np.empty((cap, 32), np.uint8)
         n = C.c_int32()
+        self._release_frame()
         self._pyr_src = None
+        self._pyr_cache = None
         self.stereo_result = None
         self._pending_image = None
         call("orbfe_extract", self._h, ptr(img), w, h, w, ptr(kps), ptr(desc), cap, C.byref(n))
@@ -144,6 +164,7 @@ class ORBextractor:
         if L.shape != R.shape:
             raise RuntimeError("left and right images differ in size")
         h, w = L.shape
+        self._release_frame()
         call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
              int(bool(want_pyramid)))
         cap = self._cap()
@@ -154,7 +175,8 @@ class ORBextractor:
             n = C.c_int32()
             call("orbfe_frame_fetch", self._h, side, ptr(kps), ptr(desc), cap, C.byref(n))
             ex._set_result(kps, desc, n.value, w > 0 and h > 0)
-            ex._pyr_src = (self._h, side) if w > 0 and h > 0 else None
+            ex._pyr_src = (self, side) if w > 0 and h > 0 else None
+            ex._pyr_cache = None
             ex.stereo_result = None
             out += [ex._kps, ex._desc]
         n = len(self._kps)
@@ -165,6 +187,7 @@ class ORBextractor:
              ptr(res["match_r"]), n, C.byref(nn))
         self.stereo_result = res
         self._stereo_partner = right_extractor
+        self._dependents = [right_extractor]
         right_extractor._pending_image = right
         return tuple(out)
 

@@ -385,3 +385,26 @@ def test_frame_results_invalidated_by_other_work():
     with pytest.raises(_lib.OrbfeError) as e:
         call("orbfe_frame_pyramid", h, 1, 2, _lib.ptr(out), C.byref(w), C.byref(hh))
     assert e.value.code == -5
+
+
+def test_right_extractor_keeps_its_pyramid_after_the_left_moves_on():
+    """the right extractor of pair 1 keeps pair 1's right pyramid after the left extractor runs
+    pair 2 with another right extractor, or a plain extract() — like the reference's independent extractors."""
+    from oracle.oracle import OracleExtractor
+    L1, R1 = synth.make_pair(21, 641, 333)
+    L2, R2 = synth.make_pair(22, 641, 333)
+    prm = dict(KITTI, nfeatures=700)
+    left, rA, rB = ORBextractor(**prm), ORBextractor(**prm), ORBextractor(**prm)
+    o = OracleExtractor(**prm)
+    o.extract(R1)
+    want = o.sheared_pyramid()
+    left.operator_kd_stereo(L1, R1, rA, BF, np.float32(FX))
+    left.operator_kd_stereo(L2, R2, rB, BF, np.float32(FX))
+    for g_, w_ in zip(rA.GetImagePyramid(), want):
+        assert np.array_equal(g_, w_)
+    left.extract(L1)
+    for g_, w_ in zip(rA.GetImagePyramid(), want):
+        assert np.array_equal(g_, w_)
+    o.extract(R2)
+    for g_, w_ in zip(rB.GetImagePyramid(), o.sheared_pyramid()):
+        assert np.array_equal(g_, w_)

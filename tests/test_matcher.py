@@ -293,3 +293,37 @@ def test_native_selection_rejects_bad_index():
                                      _lib.ptr(z), _lib.ptr(flags), _lib.ptr(z), _lib.ptr(flags), 4, 1.0, 100,
                                      _lib.ptr(out))
     assert rc < 0 and "out of range" in _lib.lib().orbfe_last_error().decode()
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_fp_python_float_xr_takes_the_float32_path(case, monkeypatch):
+    """with a Python-float mTrackProjXR and np.float32 mvuRight entries, the reference's
+    abs(XR - mvuRight[idx]) evaluates in float32 (NEP 50); the native double selection must not run then,
+    and the result must equal the Python replay's on the same inputs."""
+    from pyorbslam_amd import matcher
+    fr, mps, th, _, _ = MF.load_fp(case)
+    fr.mvuRight = [np.float32(v) if float(v) > 0 else v for v in fr.mvuRight]
+    for m in mps:
+        if m is not None and hasattr(m, "mTrackProjXR"):
+            m.mTrackProjXR = float(np.asarray(m.mTrackProjXR).ravel()[0])
+    called = []
+    orig = matcher.ORBMatcher._f_p_native
+
+    def spy(self, *a):
+        r = orig(self, *a)
+        called.append(r)
+        return r
+
+    monkeypatch.setattr(matcher.ORBMatcher, "_csr", staticmethod(cpu_csr))
+    monkeypatch.setattr(matcher.ORBMatcher, "_f_p_native", spy)
+    n_native = matcher.ORBMatcher(0.8, True).search_by_projection_f_p(fr, mps, th)
+    assert called and all(r is None for r in called)
+    got = MF.encode_fp(fr, mps)
+    fr2, mps2, th2, _, _ = MF.load_fp(case)
+    fr2.mvuRight = [np.float32(v) if float(v) > 0 else v for v in fr2.mvuRight]
+    for m in mps2:
+        if m is not None and hasattr(m, "mTrackProjXR"):
+            m.mTrackProjXR = float(np.asarray(m.mTrackProjXR).ravel()[0])
+    monkeypatch.setattr(matcher.ORBMatcher, "_f_p_native", lambda self, *a: None)
+    assert matcher.ORBMatcher(0.8, True).search_by_projection_f_p(fr2, mps2, th2) == n_native
+    assert np.array_equal(MF.encode_fp(fr2, mps2), got)

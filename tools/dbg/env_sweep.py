@@ -1,6 +1,8 @@
-"""Sweep of the per-kernel wave priorities (ORBFE_PRIO, read when a handle's geometry is built) on the
-default 4-handle bench step, one process, configurations interleaved over several rounds.
-usage: python tools/dbg/prio_sweep.py [--rounds 3] CFG [CFG ...]   (CFG = six digits r,d,o,k,b,s e.g. 002000)"""
+"""Sweep of a per-handle tuning variable read when a handle is created or reserved (ORBFE_PRIO: wave
+priorities r,d,o,k,b,s; ORBFE_STAGE_REPEAT: launches per stage r,d,o,k,s; ORBFE_OCT_KEYS ...) on the default
+4-handle bench step, one process, configurations interleaved over several rounds.
+usage: python tools/dbg/env_sweep.py [--var ORBFE_PRIO] [--rounds 3] CFG [CFG ...]
+       CFG: digits joined with commas (002000 -> "0,0,2,0,0,0"), or any string after "=" (=7424)"""
 import argparse
 import os
 import sys
@@ -13,6 +15,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--var", default="ORBFE_PRIO")
     ap.add_argument("--pairs", type=int, default=512)
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
@@ -29,7 +32,7 @@ def main():
     res = {c: [] for c in a.cfgs}
     for r in range(a.rounds):
         for c in a.cfgs:
-            os.environ["ORBFE_PRIO"] = ",".join(c)
+            os.environ[a.var] = c[1:] if c.startswith("=") else ",".join(c)
             fes = [StereoFrontEnd(max_pairs=per, lanes=1) for _ in range(a.streams)]
 
             def step():
@@ -46,10 +49,10 @@ def main():
             dt = time.perf_counter() - t0
             v = a.pairs * a.steps / dt
             res[c].append(v)
-            print(f"round {r} prio {c}: {v:.0f} pairs/s ({1e3 * dt / a.steps:.3f} ms/step)", flush=True)
+            print(f"round {r} {a.var} {c}: {v:.0f} pairs/s ({1e3 * dt / a.steps:.3f} ms/step)", flush=True)
             del fes
     for c, v in res.items():
-        print(f"prio {c}: median {sorted(v)[len(v) // 2]:.0f} pairs/s  all {[round(x) for x in v]}")
+        print(f"{a.var} {c}: median {sorted(v)[len(v) // 2]:.0f} pairs/s  all {[round(x) for x in v]}")
 
 
 if __name__ == "__main__":
