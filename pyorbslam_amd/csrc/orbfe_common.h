@@ -43,6 +43,12 @@ struct LevelGeo {
     // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
     int rs_ngrp, rs_nsrc, rs_sp;
     int64_t shear_off;   // byte offset of the level's w x h sheared view inside an image's k_shear output
+    // k_octree (bins): every candidate's quadtree path as a Morton code, code = X[x_rel] | Y[y_rel]
+    // (host tables at oct_xt / oct_yt of the octree table buffer): column in the bits above 2 * oct_d,
+    // then one 2-bit digit per depth 1 .. oct_d (x bit low, y bit high, ExtractorNode::DivideNode's
+    // quadrant).  Candidates are counted per depth-oct_d0 node (oct_bins bins, column-major).
+    int oct_d, oct_d0, oct_bins;
+    int oct_xt, oct_yt, oct_nx, oct_ny;
 };
 
 // One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.
@@ -94,6 +100,11 @@ struct Geo {
     int fd_mp;           // k_detect: u8 M map pitch in bytes (>= widest window + 6, multiple of 16)
     int fd_pq;           // k_detect: pair-queue entries (>= ceil(ww/2) * wh)
     int fd_alt;          // k_detect: largest cell slot_cap (minTh survivors staged in the ROI area)
+    int oct_bins_max;    // k_octree (bins): most bins of any level
+    int oct_tab_max;     // k_octree (bins): most X + Y table words of any level
+    int oct_kblk_max;    // k_octree (bins): most 64-key blocks of any level (key_cap / 64 + 1)
+    int oct_abl;         // k_octree_bins ablation bits (development aid, ORBFE_OCT_ABL; results are wrong when set)
+    int oct_v;           // k_octree implementation: 0 bins (default), 1 the per-candidate pass kernel (ORBFE_OCT_V)
     int prio[8];         // wave issue priority (s_setprio) per kernel, kPrio* below; 0 = default (ORBFE_PRIO)
     int umax[16];
     float scale[kMaxLevels];

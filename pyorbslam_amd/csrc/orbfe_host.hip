@@ -55,12 +55,14 @@ struct orbfe_ctx {
     std::vector<CellGeo> cells;
     std::vector<ResizeX> xt;
     std::vector<ResizeY> yt;
+    std::vector<uint32_t> octab;  // k_octree (bins): per-level Morton tables X / Y (octree_tables)
     int maxcell = 0;
 
     DevBuf<CellGeo> d_cells;
     DevBuf<ResizeX> d_xt;
     DevBuf<uint32_t> d_orb; // k_orb: horizontal items of the sample disc + centroid slots (orb_tables)
     DevBuf<ResizeY> d_yt;
+    DevBuf<uint32_t> d_octab;
     DevBuf<uint8_t> d_in;      // staging of the host-buffer API
     DevBuf<uint8_t> d_ws;
     DevBuf<int> d_cell_count;
@@ -233,6 +235,92 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
     }
 }
 
+// k_octree (bins) tables of level L (DistributeOctTree, ORBextractor.cpp:539-762).  ExtractorNode::DivideNode
+// splits a box at mx = x0 + ceil((x1 - x0) / 2), my likewise, and a key goes right / down iff x >= mx /
+// y >= my (:483-509): the x splits a key meets depend only on its column's x interval and its own x, the y
+// splits only on [0, span_y] and its y.  So a key's quadrant at every depth is a table lookup:
+// X[x_rel] = column << 2D | x bits at the even positions, Y[y_rel] = y bits at the odd positions, and
+// code = X | Y is the key's whole path in Morton order (digit q = x bit + 2 y bit at bits 2 (D - depth)).
+// D is the least depth at which every two distinct pixels of a column differ in their path, so a node of
+// depth D holds one key and is never divided.  The initial column is (int)((float)x / hX), clamped to
+// nIni - 1, and column i's box is [(int)(hX * i), (int)(hX * (i + 1))] x [0, span_y] (:543-584).
+void octree_tables(LevelGeo& L, int n_feat, std::vector<uint32_t>& tab) {
+    L.oct_d = L.oct_d0 = L.oct_bins = 0;
+    L.oct_nx = L.span_x + 1;
+    L.oct_ny = L.span_y + 1;
+    if (L.ncell == 0 || L.n_ini <= 0) {
+        L.oct_xt = L.oct_yt = (int)tab.size();
+        return;
+    }
+    constexpr int kDmax = 15;
+    auto xpath = [&](int x, int* col) {  // kDmax x bits, MSB = depth 1
+        int ci = std::min((int)((float)x / L.hx), L.n_ini - 1);
+        *col = ci;
+        int x0 = (int)(L.hx * (float)ci), x1 = (int)(L.hx * (float)(ci + 1));
+        uint32_t b = 0;
+        for (int d = 0; d < kDmax; ++d) {
+            const int mx = x0 + ((x1 - x0 + 1) >> 1);
+            const bool r = x >= mx;
+            b = (b << 1) | (uint32_t)r;
+            if (r) x0 = mx; else x1 = mx;
+        }
+        return b;
+    };
+    auto ypath = [&](int y) {
+        int y0 = 0, y1 = L.span_y;
+        uint32_t b = 0;
+        for (int d = 0; d < kDmax; ++d) {
+            const int my = y0 + ((y1 - y0 + 1) >> 1);
+            const bool r = y >= my;
+            b = (b << 1) | (uint32_t)r;
+            if (r) y0 = my; else y1 = my;
+        }
+        return b;
+    };
+    std::vector<uint32_t> xp(L.oct_nx), yp(L.oct_ny);
+    std::vector<int> xc(L.oct_nx);
+    for (int x = 0; x < L.oct_nx; ++x) xp[x] = xpath(x, &xc[x]);
+    for (int y = 0; y < L.oct_ny; ++y) yp[y] = ypath(y);
+    // least D separating neighbours (paths are monotone in x / y, so neighbours suffice)
+    int D = 1;
+    for (int x = 1; x < L.oct_nx; ++x)
+        if (xc[x] == xc[x - 1]) {
+            const uint32_t d = xp[x] ^ xp[x - 1];
+            if (!d) throw Error(ORBFE_EINVAL, "octree tables: two columns of a level share a path");
+            D = std::max(D, kDmax - (31 - __builtin_clz(d)));
+        }
+    for (int y = 1; y < L.oct_ny; ++y) {
+        const uint32_t d = yp[y] ^ yp[y - 1];
+        if (!d) throw Error(ORBFE_EINVAL, "octree tables: two rows share a path");
+        D = std::max(D, kDmax - (31 - __builtin_clz(d)));
+    }
+    int cb = 0;
+    while ((1 << cb) < L.n_ini) ++cb;
+    if (D >= kDmax || 2 * D + cb > 32) throw Error(ORBFE_EINVAL, "octree tables: level too large for 32-bit paths");
+    // bins: depth D0 with about 2 N nodes' worth of bins (the nodes the octree ends with sit at depth
+    // <= D0 on every image measured; deeper divisions take the per-candidate path of the kernel)
+    int D0 = 1;
+    while (D0 < D && (int64_t)L.n_ini << (2 * D0) < 2 * (int64_t)std::max(n_feat, 1)) ++D0;
+    while (D0 > 1 && ((int64_t)L.n_ini << (2 * D0)) > 2048) --D0;
+    L.oct_d = D;
+    L.oct_d0 = D0;
+    L.oct_bins = L.n_ini << (2 * D0);
+    L.oct_xt = (int)tab.size();
+    for (int x = 0; x < L.oct_nx; ++x) {
+        uint32_t s = 0;
+        for (int d = 1; d <= D; ++d)
+            if ((xp[x] >> (kDmax - d)) & 1u) s |= 1u << (2 * (D - d));
+        tab.push_back(((uint32_t)xc[x] << (2 * D)) | s);
+    }
+    L.oct_yt = (int)tab.size();
+    for (int y = 0; y < L.oct_ny; ++y) {
+        uint32_t s = 0;
+        for (int d = 1; d <= D; ++d)
+            if ((yp[y] >> (kDmax - d)) & 1u) s |= 1u << (2 * (D - d) + 1);
+        tab.push_back(s);
+    }
+}
+
 void build_geometry(orbfe_ctx& c, int W, int H) {
     const int L = c.prm.nlevels;
     Geo& g = c.geo;
@@ -246,6 +334,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     c.cells.clear();
     c.xt.clear();
     c.yt.clear();
+    c.octab.clear();
     c.maxcell = 0;
     int64_t ws = 0, shear = 0;
     int kp_off = 0, key_off = 0;
@@ -335,6 +424,10 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
             Lg.hx = (float)Lg.span_x / Lg.n_ini;
         }
         Lg.kp_cap = std::max(Lg.n_feat + 2, 4 * Lg.n_ini) + 2;
+        octree_tables(Lg, Lg.n_feat, c.octab);
+        g.oct_bins_max = std::max(g.oct_bins_max, Lg.oct_bins);
+        g.oct_tab_max = std::max(g.oct_tab_max, Lg.oct_nx + Lg.oct_ny);
+        g.oct_kblk_max = std::max(g.oct_kblk_max, std::min(Lg.key_cap / 64 + 1, 512));
         Lg.kp_off = kp_off;
         kp_off += Lg.kp_cap;
         g.max_ncap = std::max(g.max_ncap, Lg.kp_cap);
@@ -370,6 +463,9 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     // (very large per-level feature counts, e.g. one level with thousands of features)
     // ORBFE_PRIO=r,d,o,k,b,s: s_setprio level (0..3) of resize, detect, octree, k_orb, stereo bucket,
     // k_stereo (tuning knob for the 4-stream step; default all 0)
+    if (const char* e = std::getenv("ORBFE_OCT_V")) g.oct_v = std::atoi(e) == 1 ? 1 : 0;
+    if (const char* e = std::getenv("ORBFE_OCT_ABL")) g.oct_abl = std::atoi(e);
+    if (g.oct_v == 0 && octree_bins_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_v = 1;
     if (const char* e = std::getenv("ORBFE_PRIO")) {
         int k = 0;
         for (const char* q = e; *q && k < kPrioN; ++q)
@@ -459,6 +555,9 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.d_yt.ensure(c.yt.size());
         if (!c.yt.empty())
             HIPCK(hipMemcpy(c.d_yt.p, c.yt.data(), c.yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+        c.d_octab.ensure(std::max<size_t>(c.octab.size(), 1));
+        if (!c.octab.empty())
+            HIPCK(hipMemcpy(c.d_octab.p, c.octab.data(), c.octab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     if (max_images > c.max_images) {
         invalidate_results(c);  // the per-image buffers may move
@@ -521,8 +620,8 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
         if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
     if (prof) prof_mark(c, s, 2);
     for (int r = 0; r < c.stage_rep[2]; ++r)
-        HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, kd, kn, lvl_kp, lvl_count, c.d_overflow.p, c.maxcell, n,
-                            s));
+        HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, c.d_octab.p, kd, kn, lvl_kp, lvl_count, c.d_overflow.p,
+                            c.maxcell, n, s));
     if (prof) prof_mark(c, s, 3);
     for (int r = 0; r < c.stage_rep[3]; ++r)
         HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
@@ -1370,8 +1469,9 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                                         h->d_slots.p, n, s, variant));
                     break;
                 case 2:
-                    HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_kd.p, h->d_kn.p,
-                                        h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s, variant));
+                    HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_octab.p, h->d_kd.p,
+                                        h->d_kn.p, h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, n, s,
+                                        variant));
                     break;
                 case 3:
                     // variant 0: k_orb (production), 8: 8-wave workgroups, 12 / 9 / 10: 2 / 4 / 16 keypoints per
@@ -1457,8 +1557,9 @@ int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n) {
         DevBuf<long long> d;
         d.ensure(need);
         HIPCK(hipMemset(d.p, 0, need * sizeof(long long)));
-        HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_kd.p, h->d_kn.p, h->d_lvl_kp.p,
-                            h->d_lvl_count.p, h->d_overflow.p, h->maxcell, h->last_images, h->last_stream, 0, d.p));
+        HIPCK(launch_octree(g, h->d_cells.p, h->d_cell_count.p, h->d_slots.p, h->d_octab.p, h->d_kd.p, h->d_kn.p,
+                            h->d_lvl_kp.p, h->d_lvl_count.p, h->d_overflow.p, h->maxcell, h->last_images, h->last_stream,
+                            0, d.p));
         HIPCK(hipStreamSynchronize(h->last_stream));
         HIPCK(hipMemcpy(marks, d.p, need * sizeof(long long), hipMemcpyDeviceToHost));
     });

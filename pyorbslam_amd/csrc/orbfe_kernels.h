@@ -65,10 +65,13 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant = 0);
 size_t octree_lds_bytes(const Geo& g, int maxcell);
+size_t octree_bins_lds_bytes(const Geo& g, int maxcell);
 size_t detect_lds_bytes(const Geo& g);
-hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
-                         uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
-                         hipStream_t s, int variant = 0, long long* prof = nullptr);
+// Geo::oct_v selects k_octree_bins (0) or the per-candidate pass kernel k_octree (1); octab: the
+// per-level Morton tables of k_octree_bins (orbfe_host.hip octree_tables)
+hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots,
+                         const uint32_t* octab, uint32_t* kd, uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow,
+                         int maxcell, int n_images, hipStream_t s, int variant = 0, long long* prof = nullptr);
 // fused IC angle + 7x7 blur of each keypoint's neighbourhood + steered BRIEF (replaces k_blur + k_describe)
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,

@@ -1136,6 +1136,648 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
     else run(std::false_type{});
 }
 
+// ------------------------------------------------------------------------------- k_octree_bins
+// DistributeOctTree (ORBextractor.cpp:539-762) with the candidates counted once instead of once per pass.
+// A key's quadrant at every depth is fixed by its own x / y and the level geometry (orbfe_host.hip
+// octree_tables), so its whole path is a Morton code read from two tables, and a node of depth d is "the
+// keys whose code starts with its d digits".  One 256-thread workgroup per (image, level):
+//   1. all four waves sweep the level's candidates once (cell order = vToDistributeKeys order, each thread
+//      a contiguous run): codes from the tables (staged in LDS), a histogram over the depth-D0 nodes
+//      ("bins", column-major) and the code / response of every key into the per-image scratch;
+//   2. wave 0 scans the histogram (the key count of ANY node of depth <= D0, and of each of its four
+//      children, is then a difference of two LDS words) and runs the passes of the reference (full
+//      division, then the careful largest-first phase) on the node list only, kept in list order exactly
+//      as in k_octree (children of a pass in front in reverse creation order, surviving nodes after them
+//      in their old order);
+//   3. all waves give every key its final node (bin -> node map) and keep the first maximum response per
+//      node (response << 24 | 0xFFFFFF - key index, atomicMax); the list goes out in list order.
+// A division below depth D0 (never seen on KITTI / EuRoC / synthetic images, where the list ends at
+// depth <= 4; the host picks D0 with ~2 N bins) counts that node's children with an extra sweep of wave 0
+// over the keys of its bin.  Equal-size ties of the careful phase resolve by creation order, as in k_octree.
+constexpr int kObThreads = 256;
+constexpr int kObBatch = 8;                 // slot loads in flight per thread in the first sweep
+constexpr uint32_t kObDeep = 0x80000000u;   // bin flag: holds nodes deeper than D0 (deep sweep / final map)
+
+// LDS ordering inside wave 0's node passes (the other waves wait at a workgroup barrier meanwhile)
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (l >= o) v += y;
+    }
+    return v;
+}
+
+// Exclusive scan of a[0..n) in LDS by one wavefront (lane l owns a contiguous chunk); returns the total.
+__device__ int wave_scan_lds(int* a, int n) {
+    const int t = threadIdx.x & 63;
+    const int per = (n + 63) >> 6;
+    const int b = min(t * per, n), e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; ++i) s += a[i];
+    const int inc = wave_incl_sum(s);
+    int run = inc - s;
+    for (int i = b; i < e; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    const int tot = __shfl(inc, 63, 64);
+    wsync();
+    return tot;
+}
+
+// DPP row_shr:S (within 16-lane rows); lanes without a source lane get `old`
+template <int S>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x110 + S, 0xF, 0xF, false);
+}
+
+// One key per lane, its bin b (0xFFFFFFFF: no key) and value v = response << 24 | 0xFFFFFF - index.  Lanes
+// of a wave mostly hold consecutive keys of one cell, i.e. a few bins each held by a run of lanes, so the
+// histogram / maximum go through the run heads / tails instead of 64 same-address LDS atomics:
+// counts: the head of each run of equal bins (across the wave) adds the run length; maxima: a segmented
+// max inside each 16-lane row (idempotent, so reaching further than the run is harmless) and the last
+// lane of each run within a row applies it.
+__device__ __forceinline__ void bin_add_runs(uint32_t* hist, uint32_t* bmax, uint32_t b, uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
+    const bool valid = b != 0xFFFFFFFFu;
+    const bool head = valid && (lane == 0 || prev != b);
+    const uint64_t heads = __ballot(head) | ~__ballot(valid);  // an invalid lane also ends a run
+    if (head) {
+        const uint64_t after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+        const int next = after ? __builtin_ctzll(after) : 64;
+        atomicAdd(&hist[b], (uint32_t)(next - lane));
+    }
+    uint32_t m = v;
+    const uint32_t nob = 0xFFFFFFFEu;
+    uint32_t pb = dpp_shr<1>(nob, b), pv = dpp_shr<1>(0u, m);
+    if (pb == b) m = max(m, pv);
+    pb = dpp_shr<2>(nob, b); pv = dpp_shr<2>(0u, m);
+    if (pb == b) m = max(m, pv);
+    pb = dpp_shr<4>(nob, b); pv = dpp_shr<4>(0u, m);
+    if (pb == b) m = max(m, pv);
+    pb = dpp_shr<8>(nob, b); pv = dpp_shr<8>(0u, m);
+    if (pb == b) m = max(m, pv);
+    const uint32_t nextb = (uint32_t)__shfl_down((int)b, 1, 64);
+    const bool tail = valid && ((lane & 15) == 15 || nextb != b);
+    if (tail) atomicMax(&bmax[b], m);
+}
+
+struct ObLds {
+    uint32_t* bins;        // B + 1: histogram -> cumulative counts (bit 31: kObDeep) -> final node map
+    int *coff, *soff;      // per cell: first key index (ncell + 1), slot offset
+    uint32_t *code0, *code1;  // node list (double-buffered): left-aligned path code, key count, depth
+    int *cnt0, *cnt1;
+    uint8_t *dep0, *dep1;
+    int *sa, *sb, *sd, *sp;
+    uint64_t* srt;
+    uint32_t* c4;          // deep nodes' child counts, two u16 per word
+    int* dl;               // nodes deeper than D0 being divided / in the final list
+    uint8_t* proc;
+    uint32_t* tab;         // the level's X then Y table
+    uint32_t* bmax;        // per bin: max of (response << 24 | 0xFFFFFF - key index)
+    uint16_t* bcell;       // per 64-key block: the cell of its first key (the first oct_kblk_max blocks)
+};
+
+__host__ __device__ inline size_t ob_align(size_t v) { return (v + 15) & ~(size_t)15; }
+
+// NC node slots, B bins, CM cells, TW table words
+template <typename F>
+__host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB, F&& at) {
+    size_t o = 0;
+    auto take = [&](int id, size_t bytes) { at(id, o); o += ob_align(bytes); };
+    take(0, 4 * (size_t)(B + 1));
+    take(1, 4 * (size_t)(CM + 1));
+    take(2, 4 * (size_t)CM);
+    take(3, 4 * (size_t)NC);
+    take(4, 4 * (size_t)NC);
+    take(5, 4 * (size_t)NC);
+    take(6, 4 * (size_t)NC);
+    take(7, (size_t)NC);
+    take(8, (size_t)NC);
+    take(9, 4 * (size_t)NC);
+    take(10, 4 * (size_t)NC);
+    take(11, 4 * (size_t)NC);
+    take(12, 4 * (size_t)NC);
+    take(13, 8 * (size_t)NC);
+    take(14, 8 * (size_t)NC);
+    take(15, 4 * (size_t)NC);
+    take(16, (size_t)NC);
+    take(17, 4 * (size_t)TW);
+    take(18, 4 * (size_t)B);
+    take(19, 2 * (size_t)KB);
+    return o;
+}
+
+__global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
+                                                            const int* __restrict__ cell_count,
+                                                            const uint32_t* __restrict__ slots,
+                                                            const uint32_t* __restrict__ octab,
+                                                            uint32_t* __restrict__ code_all, uint16_t* __restrict__ resp_all,
+                                                            uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
+                                                            int* __restrict__ overflow, int maxcell,
+                                                            long long* __restrict__ prof) {
+    set_prio(g, kPrioOctree);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int s_K, s_S, s_cur, s_nd;
+    const int img = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
+    long long* pm = prof ? prof + ((int64_t)img * g.nlevels + l) * 64 : nullptr;
+    auto mark = [&](int id) {
+        if (pm && t == 0 && id < 64) pm[id] = (long long)wall_clock64();
+    };
+    mark(0);
+    const LevelGeo& L = g.lv[l];
+    const int NC = g.max_ncap;
+    ObLds d;
+    ob_carve(NC, g.oct_bins_max, maxcell, g.oct_tab_max, g.oct_kblk_max, [&](int id, size_t off) {
+        unsigned char* p = lds + off;
+        switch (id) {
+            case 0: d.bins = (uint32_t*)p; break;
+            case 1: d.coff = (int*)p; break;
+            case 2: d.soff = (int*)p; break;
+            case 3: d.code0 = (uint32_t*)p; break;
+            case 4: d.code1 = (uint32_t*)p; break;
+            case 5: d.cnt0 = (int*)p; break;
+            case 6: d.cnt1 = (int*)p; break;
+            case 7: d.dep0 = p; break;
+            case 8: d.dep1 = p; break;
+            case 9: d.sa = (int*)p; break;
+            case 10: d.sb = (int*)p; break;
+            case 11: d.sd = (int*)p; break;
+            case 12: d.sp = (int*)p; break;
+            case 13: d.srt = (uint64_t*)p; break;
+            case 14: d.c4 = (uint32_t*)p; break;
+            case 15: d.dl = (int*)p; break;
+            case 16: d.proc = p; break;
+            case 17: d.tab = (uint32_t*)p; break;
+            case 18: d.bmax = (uint32_t*)p; break;
+            default: d.bcell = (uint16_t*)p; break;
+        }
+    });
+    const int N = L.n_feat, ncell = L.ncell;
+    uint32_t* out = lvl_kp + (int64_t)img * g.lvl_kp_cap + L.kp_off;
+    int* count_out = lvl_count + img * g.nlevels + l;
+    if (ncell == 0) {
+        if (t == 0) *count_out = 0;
+        return;
+    }
+    const int D = L.oct_d, D0 = L.oct_d0, B = L.oct_bins, bsh = 2 * (D - D0);
+    const int nx = L.oct_nx, ny = L.oct_ny;
+    // ---- 1. per-cell key offsets (cell order = vToDistributeKeys order), the level's tables, empty bins
+    for (int i = t; i < ncell; i += kObThreads) {
+        d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
+        d.soff[i] = cells[L.cell0 + i].slot_off;
+    }
+    for (int i = t; i < nx + ny; i += kObThreads) d.tab[i] = octab[L.oct_xt + i];  // X then Y (adjacent)
+    for (int i = t; i <= B; i += kObThreads) d.bins[i] = 0;
+    for (int i = t; i < B; i += kObThreads) d.bmax[i] = 0;
+    __syncthreads();
+    mark(3);
+    if (t < 64) {
+        const int K = wave_scan_lds(d.coff, ncell);
+        if (t == 0) {
+            d.coff[ncell] = K;
+            s_K = K;
+        }
+    }
+    __syncthreads();
+    mark(4);
+    const int K = s_K;
+    if (K == 0) {
+        if (t == 0) *count_out = 0;
+        return;
+    }
+    // first cell of every 64-key block: the cells whose key range holds a multiple of 64 (keys past the
+    // table's Geo::oct_kblk_max blocks start from its last entry and walk further)
+    const int nblk = g.oct_kblk_max;
+    for (int c = t; c < ncell; c += kObThreads) {
+        const int a = d.coff[c], e = d.coff[c + 1];
+        for (int b = (a + 63) >> 6; (b << 6) < e && b < nblk; ++b) d.bcell[b] = (uint16_t)c;
+    }
+    __syncthreads();
+    const uint32_t* islots = slots + (int64_t)img * g.slot_total;
+    uint32_t* kcode = code_all + (int64_t)img * g.key_total + L.key_off;
+    uint16_t* kresp = resp_all + (int64_t)img * g.key_total + L.key_off;
+    const uint32_t* X = d.tab;
+    const uint32_t* Y = d.tab + nx;
+    auto key_code = [&](uint32_t v) {
+        const int x = min(max((int)(v & 0xFFFu) - kBorder, 0), nx - 1);
+        const int y = min(max((int)((v >> 12) & 0xFFFu) - kBorder, 0), ny - 1);
+        return X[x] | Y[y];
+    };
+    // keys k = t, t + 256, ... (consecutive keys in consecutive lanes: coalesced slot reads and scratch
+    // writes; both sweeps use this mapping, so a thread reads back only what it wrote itself).  A key's
+    // cell by binary search over the cell offsets, kObBatch keys' searches and slot loads in flight.
+    mark(5);
+    for (int k0 = t; k0 < K; k0 += kObThreads * kObBatch) {
+        // a key's cell: the cell of its 64-key block's first key (bcell, wave-uniform: one broadcast read),
+        // then forward over the few cells the block spans
+        int lo[kObBatch];
+#pragma unroll
+        for (int u = 0; u < kObBatch; ++u) lo[u] = d.bcell[min(min(k0 + kObThreads * u, K - 1) >> 6, nblk - 1)];
+        if (!(g.oct_abl & 1)) {
+            bool more = true;
+            while (__ballot(more)) {
+                more = false;
+#pragma unroll
+                for (int u = 0; u < kObBatch; ++u) {
+                    const bool f = d.coff[lo[u] + 1] <= k0 + kObThreads * u && k0 + kObThreads * u < K;
+                    lo[u] += f;
+                    more |= f;
+                }
+            }
+        }
+        uint32_t v[kObBatch];
+#pragma unroll
+        for (int u = 0; u < kObBatch; ++u) {
+            const int k = k0 + kObThreads * u;
+            v[u] = k < K ? ((g.oct_abl & 2) ? (uint32_t)k * 0x9E3779B1u : islots[d.soff[lo[u]] + (k - d.coff[lo[u]])]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kObBatch; ++u) {
+            const int k = k0 + kObThreads * u;
+            const uint32_t cd = key_code(v[u]);
+            if (!(g.oct_abl & 4))
+                bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v[u] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
+            if (k < K && !(g.oct_abl & 8)) {
+                kcode[k] = cd;
+                kresp[k] = (uint16_t)(v[u] >> 24);
+            }
+        }
+    }
+    mark(6);
+    __syncthreads();
+    mark(1);
+
+    // ---- 2. wave 0: cumulative counts, initial columns (:543-584), the passes (:585-737)
+    if (t < 64) {
+        wave_scan_lds((int*)d.bins, B);
+        if (t == 0) d.bins[B] = (uint32_t)K;
+        wsync();
+        auto cum = [&](int b) { return (int)(d.bins[b] & ~kObDeep); };
+        int S = 0;
+        bool ovf = false;
+        for (int i0 = 0; i0 < L.n_ini; i0 += 64) {  // empty columns removed, column order
+            const int i = i0 + t;
+            int n = 0;
+            if (i < L.n_ini) n = cum((i + 1) << (2 * D0)) - cum(i << (2 * D0));
+            const uint64_t bm = __ballot(n > 0);
+            if (n > 0) {
+                const int p = S + lanes_below(bm);
+                if (p < NC) {
+                    d.code0[p] = (uint32_t)i << (2 * D);
+                    d.cnt0[p] = n;
+                    d.dep0[p] = 0;
+                }
+            }
+            S += __popcll(bm);
+        }
+        if (S > NC) {  // cannot happen: kp_cap >= 4 nIni + 2
+            if (t == 0) atomicOr(overflow, 1);
+            S = NC;
+        }
+        wsync();
+        mark(2);
+        int C = 0, cur = 0, phase = 0;
+        bool done = false;
+        // the current list's arrays (wave-uniform selects: no dynamically indexed pointer arrays)
+        auto L_code = [&]() { return cur ? d.code1 : d.code0; };
+        auto L_cnt = [&]() { return cur ? d.cnt1 : d.cnt0; };
+        auto L_dep = [&]() { return cur ? d.dep1 : d.dep0; };
+        // the four children's key counts of node p of the current list
+        auto child_counts = [&](int p) {
+            const int dp = L_dep()[p];
+            int4 cc;
+            if (dp < D0) {
+                const int lo = (int)(L_code()[p] >> bsh), w = 1 << (2 * (D0 - dp - 1));
+                const int c0 = cum(lo), c1 = cum(lo + w), c2 = cum(lo + 2 * w), c3 = cum(lo + 3 * w), c4 = cum(lo + 4 * w);
+                cc = int4{c1 - c0, c2 - c1, c3 - c2, c4 - c3};
+            } else {
+                const uint32_t a = d.c4[2 * p], b = d.c4[2 * p + 1];
+                cc = int4{(int)(a & 0xFFFFu), (int)(a >> 16), (int)(b & 0xFFFFu), (int)(b >> 16)};
+            }
+            return cc;
+        };
+        auto cc_at = [](const int4& cc, int q) { return q == 0 ? cc.x : q == 1 ? cc.y : q == 2 ? cc.z : cc.w; };
+        // children counts of the nodes deeper than D0 among those that may divide (sel(p), p < nsel): one
+        // sweep of wave 0 over the keys (scratch codes written by every thread: read at device scope)
+        auto deep_counts = [&](int nsel, auto&& sel) {
+            int nd = 0;
+            for (int p0 = 0; p0 < nsel; p0 += 64) {
+                const int p = p0 + t;
+                const bool deep = p < nsel && sel(p) && L_dep()[p] >= D0;
+                const uint64_t bm = __ballot(deep);
+                if (deep) {
+                    d.dl[nd + lanes_below(bm)] = p;
+                    d.c4[2 * p] = 0u;
+                    d.c4[2 * p + 1] = 0u;
+                    atomicOr(&d.bins[L_code()[p] >> bsh], kObDeep);
+                }
+                nd += __popcll(bm);
+            }
+            if (nd == 0) return;
+            wsync();
+            const uint32_t* code = L_code();
+            const uint8_t* dep = L_dep();
+            for (int k = t; k < K; k += 64) {
+                const uint32_t cd = __hip_atomic_load(kcode + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(d.bins[cd >> bsh] & kObDeep)) continue;
+                for (int i = 0; i < nd; ++i) {
+                    const int p = d.dl[i], dp = dep[p];
+                    if (((cd ^ code[p]) >> (2 * (D - dp))) == 0u) {
+                        const int q = (int)((cd >> (2 * (D - dp - 1))) & 3u);
+                        atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
+                        break;
+                    }
+                }
+            }
+            wsync();
+            for (int i = t; i < nd; i += 64) atomicAnd(&d.bins[L_code()[d.dl[i]] >> bsh], ~kObDeep);
+            wsync();
+        };
+        auto put = [&](int np, uint32_t code, int n, int dp) {
+            if (np < NC) {
+                (cur ? d.code0 : d.code1)[np] = code;
+                (cur ? d.cnt0 : d.cnt1)[np] = n;
+                (cur ? d.dep0 : d.dep1)[np] = (uint8_t)dp;
+            } else {
+                ovf = true;
+            }
+        };
+
+        for (int iter = 0; !done; ++iter) {
+            if (iter > 4 * NC + 64) {  // cannot happen (each pass grows the list or finishes); never hang
+                if (t == 0) atomicOr(overflow, 2);
+                break;
+            }
+            mark(8 + 4 * iter);
+            const uint32_t* code = L_code();
+            const int* cnt = L_cnt();
+            const uint8_t* dep = L_dep();
+            if (phase == 0) {
+                // ---------------- full pass (:605-664): divide every node holding more than one key
+                deep_counts(S, [&](int p) { return cnt[p] > 1; });
+                int nexp = 0;
+                for (int p = t; p < S; p += 64) {
+                    int nc = 0;
+                    if (cnt[p] > 1) {
+                        const int4 cc = child_counts(p);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            nc += cc_at(cc, q) > 0;
+                            nexp += cc_at(cc, q) > 1;
+                        }
+                    }
+                    d.sa[p] = nc;
+                    d.sb[p] = cnt[p] == 1;
+                }
+                wsync();
+                const int Cn = wave_scan_lds(d.sa, S);
+                const int Kk = wave_scan_lds(d.sb, S);
+                nexp = __shfl(wave_incl_sum(nexp), 63, 64);
+                for (int p = t; p < S; p += 64) {
+                    if (cnt[p] > 1) {
+                        const int4 cc = child_counts(p);
+                        int c = d.sa[p];
+                        const int dp = dep[p];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (cc_at(cc, q) > 0)
+                                put(Cn - 1 - c++, code[p] | ((uint32_t)q << (2 * (D - dp - 1))), cc_at(cc, q), dp + 1);
+                    } else {
+                        put(Cn + d.sb[p], code[p], cnt[p], dep[p]);
+                    }
+                }
+                wsync();
+                const int Sn = Cn + Kk;
+                if (Sn > NC) {
+                    ovf = true;
+                    done = true;
+                } else if (Sn >= N || Sn == S) {
+                    done = true;                                     // :668-671
+                } else if (Sn + 3 * nexp > N) {
+                    phase = 1;                                       // :672
+                }
+                S = min(Sn, NC);
+                C = min(Cn, NC);
+                cur ^= 1;
+            } else {
+                // ---------------- careful phase (:675-736): divide the largest nodes of the last step first
+                deep_counts(C, [&](int p) { return cnt[p] > 1; });
+                // candidates (position order) -> ranked by size desc, then position asc (creation desc)
+                int M = 0, big = 0;
+                for (int p0 = 0; p0 < C; p0 += 64) {
+                    const int p = p0 + t;
+                    const bool cand = p < C && cnt[p] > 1;
+                    const uint64_t bm = __ballot(cand);
+                    if (cand) {
+                        d.srt[M + lanes_below(bm)] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
+                        big |= cnt[p] > 0xFFFF;
+                    }
+                    M += __popcll(bm);
+                }
+                for (int p = t; p < S; p += 64) d.proc[p] = 0;
+                wsync();
+                mark(9 + 4 * iter);
+                // rank = #{larger (size, -position)}: size desc, then position asc (creation desc).  Keys are
+                // unique; 4 candidates per lane against every candidate (LDS broadcast reads, 8 in flight),
+                // as 32-bit keys (size << 16 | 0xFFFF - position) when every size and position fits 16 bits
+                if (!__ballot(big) && NC <= 0x10000) {
+                    uint32_t* k32 = (uint32_t*)d.sd;
+                    for (int i = t; i < M; i += 64) {
+                        const uint64_t v = d.srt[i];
+                        k32[i] = ((uint32_t)(v >> 32) << 16) | (0xFFFFu - (0xFFFFFFFFu - (uint32_t)v));
+                    }
+                    wsync();
+                    for (int i0 = 0; i0 < M; i0 += 256) {
+                        uint32_t v[4];
+                        int r[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int i = i0 + 64 * u + t;
+                            v[u] = i < M ? k32[i] : 0u;
+                            r[u] = 0;
+                        }
+                        int j = 0;
+                        for (; j + 8 <= M; j += 8) {
+                            uint32_t w[8];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) w[e] = k32[j + e];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e)
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) r[u] += w[e] > v[u];
+                        }
+                        for (; j < M; ++j) {
+                            const uint32_t w = k32[j];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) r[u] += w > v[u];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (i0 + 64 * u + t < M) d.sp[r[u]] = (int)(0xFFFFu - (v[u] & 0xFFFFu));
+                    }
+                } else {
+                    for (int i0 = 0; i0 < M; i0 += 256) {
+                        uint64_t v[4];
+                        int r[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int i = i0 + 64 * u + t;
+                            v[u] = i < M ? d.srt[i] : 0;
+                            r[u] = 0;
+                        }
+                        for (int j = 0; j < M; ++j) {
+                            const uint64_t w = d.srt[j];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) r[u] += w > v[u];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (i0 + 64 * u + t < M) d.sp[r[u]] = (int)(0xFFFFFFFFu - (uint32_t)v[u]);
+                    }
+                }
+                wsync();
+                mark(10 + 4 * iter);
+                for (int j = t; j < M; j += 64) {
+                    const int4 cc = child_counts(d.sp[j]);
+                    const int nc = (cc.x > 0) + (cc.y > 0) + (cc.z > 0) + (cc.w > 0);
+                    d.sb[j] = nc - 1;
+                    d.sd[j] = nc;
+                }
+                wsync();
+                wave_scan_lds(d.sb, M);
+                int pmin = 0x7fffffff;
+                for (int j = t; j < M; j += 64)
+                    if (S + d.sb[j] + d.sd[j] - 1 >= N) pmin = min(pmin, j);  // :729-730 break
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) pmin = min(pmin, __shfl_xor(pmin, o, 64));
+                const int P = pmin == 0x7fffffff ? M : pmin + 1;
+                for (int j = t; j < M; j += 64) {
+                    if (j >= P) d.sd[j] = 0;
+                    else d.proc[d.sp[j]] = 1;
+                }
+                wsync();
+                const int Cn = wave_scan_lds(d.sd, M);
+                for (int p = t; p < S; p += 64) d.sa[p] = d.proc[p] == 0;
+                wsync();
+                const int Kk = wave_scan_lds(d.sa, S);
+                for (int j = t; j < P; j += 64) {
+                    const int p = d.sp[j];
+                    const int4 cc = child_counts(p);
+                    int c = d.sd[j];
+                    const int dp = dep[p];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (cc_at(cc, q) > 0)
+                            put(Cn - 1 - c++, code[p] | ((uint32_t)q << (2 * (D - dp - 1))), cc_at(cc, q), dp + 1);
+                }
+                for (int p = t; p < S; p += 64)
+                    if (!d.proc[p]) put(Cn + d.sa[p], code[p], cnt[p], dep[p]);
+                wsync();
+                const int Sn = Cn + Kk;
+                if (Sn > NC) ovf = true;
+                if (Sn > NC || Sn >= N || Sn == S) done = true;  // :733-734
+                S = min(Sn, NC);
+                C = min(Cn, NC);
+                cur ^= 1;
+            }
+        }
+        if (__ballot(ovf) && t == 0) atomicOr(overflow, 4);
+        // nodes deeper than D0 of the final list, for the final map
+        const uint8_t* dep = L_dep();
+        int nd = 0;
+        for (int p0 = 0; p0 < S; p0 += 64) {
+            const int p = p0 + t;
+            const bool deep = p < S && dep[p] > D0;
+            const uint64_t bm = __ballot(deep);
+            if (deep) d.dl[nd + lanes_below(bm)] = p;
+            nd += __popcll(bm);
+        }
+        if (t == 0) {
+            s_S = S;
+            s_cur = cur;
+            s_nd = nd;
+        }
+    }
+    __syncthreads();
+    mark(60);
+
+    // ---- 3. the first maximum-response key of every node (:740-759), list order
+    const int S = s_S, nd = s_nd;
+    const uint32_t* code = s_cur ? d.code1 : d.code0;
+    const uint8_t* dep = s_cur ? d.dep1 : d.dep0;
+    uint32_t* best = (uint32_t*)d.sa;
+    // a node of depth <= D0 covers whole bins: its best key is the maximum of their maxima
+    for (int p = t; p < S; p += kObThreads) {
+        const int dp = dep[p];
+        const int lo = (int)(code[p] >> bsh);
+        uint32_t m = 0u;
+        if (dp <= D0) {
+            const int w = 1 << (2 * (D0 - dp));
+            for (int b = lo; b < lo + w; ++b) m = max(m, d.bmax[b]);
+        }
+        best[p] = m;
+    }
+    __syncthreads();
+    // nodes deeper than D0 (rare): a sweep over the keys of their bins (bin flag, then a prefix match)
+    if (nd > 0) {
+        for (int i = t; i < nd; i += kObThreads) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
+        __syncthreads();
+    }
+    for (int k0 = t; nd > 0 && k0 < K; k0 += kObThreads * kObBatch) {  // the first sweep's keys: the thread's own writes
+        uint32_t cd[kObBatch], rs[kObBatch];
+#pragma unroll
+        for (int u = 0; u < kObBatch; ++u) {
+            const int k = k0 + kObThreads * u;
+            cd[u] = k < K ? kcode[k] : 0u;
+            rs[u] = k < K ? kresp[k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kObBatch; ++u) {
+            const int k = k0 + kObThreads * u;
+            if (k >= K) continue;
+            uint32_t p = 0xFFFFFFFFu;
+            if (d.bins[cd[u] >> bsh] == kObDeep) {
+                for (int i = 0; i < nd; ++i) {
+                    const int q = d.dl[i];
+                    if (((cd[u] ^ code[q]) >> (2 * (D - dep[q]))) == 0u) {
+                        p = (uint32_t)q;
+                        break;
+                    }
+                }
+            }
+            if (p < (uint32_t)S) atomicMax(&best[p], (rs[u] << 24) | (0xFFFFFFu - (uint32_t)k));
+        }
+    }
+    __syncthreads();
+    for (int p = t; p < S; p += kObThreads) {
+        const uint32_t bv = best[p];
+        const int k = 0xFFFFFF - (int)(bv & 0xFFFFFFu);
+        if (bv != 0u && k < K) {
+            int lo = 0, hi = ncell - 1;  // last cell with coff <= k
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
+            }
+            out[p] = islots[d.soff[lo] + (k - d.coff[lo])];
+        } else {  // a node without keys cannot occur; flag instead of reading out of range
+            out[p] = 0u;
+            atomicOr(overflow, 16);
+        }
+    }
+    if (t == 0) *count_out = S;
+    mark(63);
+}
+
 // ------------------------------------------------------------------------------- descriptor math
 // glibc 2.35 x86-64 sinf / cosf (FMA ifunc variant; ARM optimized-routines algorithm), |x| < 120.
 // glibc's two coefficient tables differ only in the sign of the cosine coefficients, so the second
@@ -2029,9 +2671,24 @@ size_t octree_lds_bytes(const Geo& g, int maxcell) {
            6 * (size_t)g.oct_keys;
 }
 
-hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots, uint32_t* kd,
-                         uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow, int maxcell, int n_images,
-                         hipStream_t s, int variant, long long* prof) {
+size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
+    return ob_carve(g.max_ncap, g.oct_bins_max, maxcell, g.oct_tab_max, g.oct_kblk_max, [](int, size_t) {});
+}
+
+hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots,
+                         const uint32_t* octab, uint32_t* kd, uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow,
+                         int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
+    if (g.oct_v == 0) {
+        const size_t lds = octree_bins_lds_bytes(g, maxcell);
+        if (lds > 64 * 1024) {
+            const hipError_t e =
+                hipFuncSetAttribute((const void*)k_octree_bins, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_octree_bins, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells, cell_count, slots,
+                           octab, kd, kn, lvl_kp, lvl_count, overflow, maxcell, prof);
+        return hipGetLastError();
+    }
     const size_t lds = octree_lds_bytes(g, maxcell);
     if (lds > 64 * 1024) {  // gfx950: up to 160 KiB per workgroup, above 64 KiB on request
         const hipError_t e = hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -12,6 +12,7 @@ from pyorbslam_amd._lib import call, ptr
 from pyorbslam_amd.pyORBExtractor import ORBextractor
 
 pytestmark = pytest.mark.gpu
+NAMES = ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd", "patch", "clusters"]
 
 
 def _images(kitti_png):
@@ -21,8 +22,16 @@ def _images(kitti_png):
     noise = rng.integers(0, 256, (376, 1241)).astype(np.uint8)
     small = synth.make_pair(9, 211, 157)[0]
     odd = synth.make_pair(11, 641, 333)[1]
+    # octree stress: every candidate of a level inside one small patch (the list divides far below the
+    # depth k_octree_bins keeps bins for), and a few dense clusters on a flat image
+    patch = np.full((376, 1241), 90, np.uint8)
+    patch[170:202, 600:632] = rng.integers(0, 256, (32, 32))
+    clusters = np.full((376, 1241), 120, np.uint8)
+    for cy, cx in ((60, 100), (64, 130), (300, 1100), (200, 640), (205, 655)):
+        clusters[cy:cy + 14, cx:cx + 14] = rng.integers(0, 256, (14, 14))
     return {"kitti_L": (L0, KITTI), "kitti_R": (R0, KITTI), "kitti06": (kitti_png, KITTI), "euroc": (Le, EUROC),
-            "noise": (noise, KITTI), "small": (small, dict(KITTI, nfeatures=500)), "odd": (odd, KITTI)}
+            "noise": (noise, KITTI), "small": (small, dict(KITTI, nfeatures=500)), "odd": (odd, KITTI),
+            "patch": (patch, KITTI), "clusters": (clusters, KITTI)}
 
 
 def _debug(ex, fn, level, cap=400000):
@@ -52,7 +61,7 @@ def cases(kitti_png):
     return out
 
 
-@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+@pytest.mark.parametrize("name", NAMES)
 def test_pyramid(cases, name):
     img, params, ex, *_rest = cases[name]
     orc = cases[name][5]
@@ -62,7 +71,7 @@ def test_pyramid(cases, name):
         assert np.array_equal(g, o), f"sheared level {l}"
 
 
-@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+@pytest.mark.parametrize("name", NAMES)
 def test_fast_cells(cases, name):
     img, params, ex, kps, desc, orc, okps, odesc = cases[name]
     p = O.Params(params["nfeatures"], params["scaleFactor"], params["nlevels"], params["iniThFAST"],
@@ -75,7 +84,7 @@ def test_fast_cells(cases, name):
         assert a is None, f"level {l} first diff at {i}: {a} vs {b}"
 
 
-@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+@pytest.mark.parametrize("name", NAMES)
 def test_octree(cases, name):
     img, params, ex, kps, desc, orc, okps, odesc = cases[name]
     npl = ex.features_per_level()
@@ -89,7 +98,7 @@ def test_octree(cases, name):
         assert a is None, f"level {l} first diff at {i}: {a} vs {b}"
 
 
-@pytest.mark.parametrize("name", ["kitti_L", "kitti_R", "kitti06", "euroc", "noise", "small", "odd"])
+@pytest.mark.parametrize("name", NAMES)
 def test_keypoints_and_descriptors_bit_exact(cases, name):
     img, params, ex, kps, desc, orc, okps, odesc = cases[name]
     assert len(kps) == len(okps)
