@@ -398,57 +398,49 @@ def max_over_ranks(v, dev, world):
 
 
 def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
-    """The shard's pairs streamed from pinned host memory every step: H2D of the images on a copy stream
-    into one of two device buffers while the handles compute on the other; after its batch each handle
-    packs its pairs' records (k_pack) and a second copy stream brings them back D2H into pinned memory.
-    Timed like a step (barrier + synchronize, max over ranks).  The records of the last step are checked
-    against the handles' own results."""
+    """The shard's pairs streamed from pinned host memory every step, per handle: its images H2D on a copy
+    stream into one of two device buffers (the handle starts as soon as ITS chunk has landed, while the
+    next chunks are still on the link), its batch, its pairs' records packed (k_pack) and brought back D2H
+    into pinned memory on a second copy stream.  Timed like a step (barrier + synchronize, max over ranks);
+    the records of the last step are checked against the handles' own results."""
     import torch
     from pyorbslam_amd import dist as D
     from pyorbslam_amd._lib import call
     n = sh.n_pairs
+    H = len(sh.fes)
     hin = torch.from_numpy(host).pin_memory()
     dbuf = [torch.empty(hin.shape, dtype=torch.uint8, device=dev) for _ in range(2)]
     rb = D.record_bytes(sh.fes[0].kp_cap)
     drec = [torch.empty((n, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
     hrec = [torch.empty((n, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
     h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    ev_in = [torch.cuda.Event() for _ in range(2)]
-    ev_free = [[torch.cuda.Event() for _ in sh.fes] for _ in range(2)]   # handle j done reading dbuf[b]
-    ev_out = [torch.cuda.Event() for _ in range(2)]                      # D2H of drec[b] done
+    ev = {name: [[torch.cuda.Event() for _ in range(H)] for _ in range(2)] for name in ("in", "free", "out")}
+    offs = np.concatenate([[0], np.cumsum(sh.counts)]).tolist()
     it = [0]
-    used = [[False, False], [False, False]]  # [b][0]: ev_free recorded, [b][1]: ev_out recorded
+    seen = [False, False]  # buffer b has been used once: its events were recorded
 
     def step():
         b = it[0] % 2
         it[0] += 1
-        with torch.cuda.stream(h2d):
-            if used[b][0]:
-                for e in ev_free[b]:
-                    h2d.wait_event(e)
-            dbuf[b].copy_(hin, non_blocking=True)
-            ev_in[b].record(h2d)
-        subs, o = [], 0
-        for c in sh.counts:
-            subs.append(dbuf[b][2 * o: 2 * (o + c)])
-            o += c
-        o = 0
-        for j, (f, st, sub, c) in enumerate(zip(sh.fes, sh.streams, subs, sh.counts)):
-            st.wait_event(ev_in[b])
-            if used[b][1]:
-                st.wait_event(ev_out[b])   # drec[b] of two steps ago has left the device
-            f.enqueue(sub, c, stream_ptr=st.cuda_stream)
-            call("orbfe_batch_pack_device", f.handle, C.c_void_p(drec[b][o].data_ptr()), rb, 0, c,
+        for j, (f, st, c) in enumerate(zip(sh.fes, sh.streams, sh.counts)):
+            o0, o1 = offs[j], offs[j + 1]
+            with torch.cuda.stream(h2d):
+                if seen[b]:
+                    h2d.wait_event(ev["free"][b][j])   # handle j finished reading dbuf[b] two steps ago
+                dbuf[b][2 * o0:2 * o1].copy_(hin[2 * o0:2 * o1], non_blocking=True)
+                ev["in"][b][j].record(h2d)
+            st.wait_event(ev["in"][b][j])
+            if seen[b]:
+                st.wait_event(ev["out"][b][j])         # drec[b] rows of handle j have left the device
+            f.enqueue(dbuf[b][2 * o0:2 * o1], c, stream_ptr=st.cuda_stream)
+            call("orbfe_batch_pack_device", f.handle, C.c_void_p(drec[b][o0].data_ptr()), rb, 0, c,
                  C.c_void_p(st.cuda_stream))
-            ev_free[b][j].record(st)
-            o += c
-        used[b][0] = True
-        with torch.cuda.stream(d2h):
-            for e in ev_free[b]:
-                d2h.wait_event(e)
-            hrec[b].copy_(drec[b], non_blocking=True)
-            ev_out[b].record(d2h)
-        used[b][1] = True
+            ev["free"][b][j].record(st)
+            with torch.cuda.stream(d2h):
+                d2h.wait_event(ev["free"][b][j])
+                hrec[b][o0:o1].copy_(drec[b][o0:o1], non_blocking=True)
+                ev["out"][b][j].record(d2h)
+        seen[b] = True
 
     el = timed(step, steps, warmup, dev, world)
     last = (it[0] - 1) % 2
@@ -467,9 +459,10 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
             "h2d_GBs_per_gpu": round(in_b * steps / el / 1e9, 2), "d2h_GBs_per_gpu": round(out_b * steps / el / 1e9, 2),
             "pcie_bound_pairs_per_s_per_gpu": round(PCIE_PEAK_GBS * 1e9 / (in_b / n), 1),
             "record_check": ok,
-            "what": "images H2D from pinned host memory every step (copy stream, two device buffers) overlapped "
-                    "with compute, every pair's packed record D2H into pinned memory (second copy stream); "
-                    "PCIe Gen5 x16 spec 63 GB/s per direction bounds the H2D leg"}
+            "what": "per handle: its images H2D from pinned host memory (copy stream, two device buffers), its batch, "
+                    "its pairs' packed records D2H into pinned memory (second copy stream); chunks of later handles "
+                    "stream while earlier handles compute; PCIe Gen5 x16 spec 63 GB/s per direction bounds the H2D "
+                    "leg (tools/dbg/pcie_probe.py measured 57 GB/s H2D alone, 45 GB/s with the D2H leg running)"}
 
 
 # ----------------------------------------------------------------------------------- evidence lookups

@@ -1155,7 +1155,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
 // depth <= 4; the host picks D0 with ~2 N bins) counts that node's children with an extra sweep of wave 0
 // over the keys of its bin.  Equal-size ties of the careful phase resolve by creation order, as in k_octree.
 constexpr int kObThreads = 256;
-constexpr int kObBatch = 8;                 // slot loads in flight per thread in the first sweep
+#ifndef ORBFE_OB_BATCH
+#define ORBFE_OB_BATCH 8
+#endif
+constexpr int kObBatch = ORBFE_OB_BATCH;    // slot loads in flight per thread in the first sweep
 constexpr uint32_t kObDeep = 0x80000000u;   // bin flag: holds nodes deeper than D0 (deep sweep / final map)
 
 // LDS ordering inside wave 0's node passes (the other waves wait at a workgroup barrier meanwhile)
@@ -1573,30 +1576,30 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
                 // ---------------- careful phase (:675-736): divide the largest nodes of the last step first
                 deep_counts(C, [&](int p) { return cnt[p] > 1; });
                 // candidates (position order) -> ranked by size desc, then position asc (creation desc)
-                int M = 0, big = 0;
+                // keys: size desc, then position asc (creation desc); unique.  32-bit (size << 16 |
+                // 0xFFFF - position) when every size and position fits 16 bits, else 64-bit
+                int bigl = 0;
+                for (int p = t; p < C; p += 64) bigl |= cnt[p] > 0xFFFF;
+                const bool k32path = !__ballot(bigl) && NC <= 0x10000;
+                uint32_t* k32 = (uint32_t*)d.srt;
+                int M = 0;
                 for (int p0 = 0; p0 < C; p0 += 64) {
                     const int p = p0 + t;
                     const bool cand = p < C && cnt[p] > 1;
                     const uint64_t bm = __ballot(cand);
                     if (cand) {
-                        d.srt[M + lanes_below(bm)] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
-                        big |= cnt[p] > 0xFFFF;
+                        const int m = M + lanes_below(bm);
+                        if (k32path) k32[m] = ((uint32_t)cnt[p] << 16) | (0xFFFFu - (uint32_t)p);
+                        else d.srt[m] = ((uint64_t)(uint32_t)cnt[p] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
                     }
                     M += __popcll(bm);
                 }
                 for (int p = t; p < S; p += 64) d.proc[p] = 0;
                 wsync();
                 mark(9 + 4 * iter);
-                // rank = #{larger (size, -position)}: size desc, then position asc (creation desc).  Keys are
-                // unique; 4 candidates per lane against every candidate (LDS broadcast reads, 8 in flight),
-                // as 32-bit keys (size << 16 | 0xFFFF - position) when every size and position fits 16 bits
-                if (!__ballot(big) && NC <= 0x10000) {
-                    uint32_t* k32 = (uint32_t*)d.sd;
-                    for (int i = t; i < M; i += 64) {
-                        const uint64_t v = d.srt[i];
-                        k32[i] = ((uint32_t)(v >> 32) << 16) | (0xFFFFu - (0xFFFFFFFFu - (uint32_t)v));
-                    }
-                    wsync();
+                if (k32path) {
+                    // rank = #{larger key}: 4 candidates per lane against every candidate (LDS broadcast reads,
+                    // 8 in flight; a bitonic sort in LDS measured slower: 36 dependent stages for M ~ 200)
                     for (int i0 = 0; i0 < M; i0 += 256) {
                         uint32_t v[4];
                         int r[4];
@@ -1626,6 +1629,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
                             if (i0 + 64 * u + t < M) d.sp[r[u]] = (int)(0xFFFFu - (v[u] & 0xFFFFu));
                     }
                 } else {
+                    // rank = #{larger key}: 4 candidates per lane against every candidate (broadcast reads)
                     for (int i0 = 0; i0 < M; i0 += 256) {
                         uint64_t v[4];
                         int r[4];
