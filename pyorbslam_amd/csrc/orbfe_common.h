@@ -103,7 +103,6 @@ struct Geo {
     int oct_bins_max;    // k_octree (bins): most bins of any level
     int oct_tab_max;     // k_octree (bins): most X + Y table words of any level
     int oct_kblk_max;    // k_octree (bins): most 64-key blocks of any level (key_cap / 64 + 1)
-    int oct_abl;         // k_octree_bins ablation bits (development aid, ORBFE_OCT_ABL; results are wrong when set)
     int oct_v;           // k_octree implementation: 0 bins (default), 1 the per-candidate pass kernel (ORBFE_OCT_V)
     int prio[8];         // wave issue priority (s_setprio) per kernel, kPrio* below; 0 = default (ORBFE_PRIO)
     int umax[16];

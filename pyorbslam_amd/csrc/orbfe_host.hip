@@ -297,10 +297,11 @@ void octree_tables(LevelGeo& L, int n_feat, std::vector<uint32_t>& tab) {
     int cb = 0;
     while ((1 << cb) < L.n_ini) ++cb;
     if (D >= kDmax || 2 * D + cb > 32) throw Error(ORBFE_EINVAL, "octree tables: level too large for 32-bit paths");
-    // bins: depth D0 with about 2 N nodes' worth of bins (the nodes the octree ends with sit at depth
-    // <= D0 on every image measured; deeper divisions take the per-candidate path of the kernel)
+    // bins: depth D0 with about 8 N nodes' worth of bins, at most 2048 (the nodes the octree ends with sit
+    // at depth <= 4 on every KITTI / EuRoC / synthetic image measured; deeper divisions take the
+    // per-candidate path of the kernel)
     int D0 = 1;
-    while (D0 < D && (int64_t)L.n_ini << (2 * D0) < 2 * (int64_t)std::max(n_feat, 1)) ++D0;
+    while (D0 < D && (int64_t)L.n_ini << (2 * D0) < 8 * (int64_t)std::max(n_feat, 1)) ++D0;
     while (D0 > 1 && ((int64_t)L.n_ini << (2 * D0)) > 2048) --D0;
     L.oct_d = D;
     L.oct_d0 = D0;
@@ -464,7 +465,6 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     // ORBFE_PRIO=r,d,o,k,b,s: s_setprio level (0..3) of resize, detect, octree, k_orb, stereo bucket,
     // k_stereo (tuning knob for the 4-stream step; default all 0)
     if (const char* e = std::getenv("ORBFE_OCT_V")) g.oct_v = std::atoi(e) == 1 ? 1 : 0;
-    if (const char* e = std::getenv("ORBFE_OCT_ABL")) g.oct_abl = std::atoi(e);
     if (g.oct_v == 0 && octree_bins_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_v = 1;
     if (const char* e = std::getenv("ORBFE_PRIO")) {
         int k = 0;

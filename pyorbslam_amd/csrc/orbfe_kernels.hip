@@ -1284,7 +1284,6 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
                                                             const int* __restrict__ cell_count,
                                                             const uint32_t* __restrict__ slots,
                                                             const uint32_t* __restrict__ octab,
-                                                            uint32_t* __restrict__ code_all, uint16_t* __restrict__ resp_all,
                                                             uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
                                                             int* __restrict__ overflow, int maxcell,
                                                             long long* __restrict__ prof) {
@@ -1367,8 +1366,6 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     }
     __syncthreads();
     const uint32_t* islots = slots + (int64_t)img * g.slot_total;
-    uint32_t* kcode = code_all + (int64_t)img * g.key_total + L.key_off;
-    uint16_t* kresp = resp_all + (int64_t)img * g.key_total + L.key_off;
     const uint32_t* X = d.tab;
     const uint32_t* Y = d.tab + nx;
     auto key_code = [&](uint32_t v) {
@@ -1379,43 +1376,38 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     // keys k = t, t + 256, ... (consecutive keys in consecutive lanes: coalesced slot reads and scratch
     // writes; both sweeps use this mapping, so a thread reads back only what it wrote itself).  A key's
     // cell by binary search over the cell offsets, kObBatch keys' searches and slot loads in flight.
-    mark(5);
-    for (int k0 = t; k0 < K; k0 += kObThreads * kObBatch) {
-        // a key's cell: the cell of its 64-key block's first key (bcell, wave-uniform: one broadcast read),
-        // then forward over the few cells the block spans
-        int lo[kObBatch];
+    // Every key once: keys k = tid, tid + nthr, ... (consecutive keys in consecutive lanes: coalesced slot
+    // reads), kObBatch of them in flight per thread; a key's cell is the cell of its 64-key block's first key
+    // (bcell) walked forward over the few cells the block spans.  fn(k, slot value, code) for k < K.
+    auto for_keys = [&](int tid, int nthr, auto&& fn) {
+        for (int k0 = tid; k0 < K; k0 += nthr * kObBatch) {
+            int lo[kObBatch];
 #pragma unroll
-        for (int u = 0; u < kObBatch; ++u) lo[u] = d.bcell[min(min(k0 + kObThreads * u, K - 1) >> 6, nblk - 1)];
-        if (!(g.oct_abl & 1)) {
+            for (int u = 0; u < kObBatch; ++u) lo[u] = d.bcell[min(min(k0 + nthr * u, K - 1) >> 6, nblk - 1)];
             bool more = true;
             while (__ballot(more)) {
                 more = false;
 #pragma unroll
                 for (int u = 0; u < kObBatch; ++u) {
-                    const bool f = d.coff[lo[u] + 1] <= k0 + kObThreads * u && k0 + kObThreads * u < K;
+                    const bool f = d.coff[lo[u] + 1] <= k0 + nthr * u && k0 + nthr * u < K;
                     lo[u] += f;
                     more |= f;
                 }
             }
-        }
-        uint32_t v[kObBatch];
+            uint32_t v[kObBatch];
 #pragma unroll
-        for (int u = 0; u < kObBatch; ++u) {
-            const int k = k0 + kObThreads * u;
-            v[u] = k < K ? ((g.oct_abl & 2) ? (uint32_t)k * 0x9E3779B1u : islots[d.soff[lo[u]] + (k - d.coff[lo[u]])]) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kObBatch; ++u) {
-            const int k = k0 + kObThreads * u;
-            const uint32_t cd = key_code(v[u]);
-            if (!(g.oct_abl & 4))
-                bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v[u] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
-            if (k < K && !(g.oct_abl & 8)) {
-                kcode[k] = cd;
-                kresp[k] = (uint16_t)(v[u] >> 24);
+            for (int u = 0; u < kObBatch; ++u) {
+                const int k = k0 + nthr * u;
+                v[u] = k < K ? islots[d.soff[lo[u]] + (k - d.coff[lo[u]])] : 0u;
             }
+#pragma unroll
+            for (int u = 0; u < kObBatch; ++u) fn(k0 + nthr * u, v[u], key_code(v[u]));
         }
-    }
+    };
+    mark(5);
+    for_keys(t, kObThreads, [&](int k, uint32_t v, uint32_t cd) {
+        bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
+    });
     mark(6);
     __syncthreads();
     mark(1);
@@ -1490,9 +1482,8 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
             wsync();
             const uint32_t* code = L_code();
             const uint8_t* dep = L_dep();
-            for (int k = t; k < K; k += 64) {
-                const uint32_t cd = __hip_atomic_load(kcode + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!(d.bins[cd >> bsh] & kObDeep)) continue;
+            for_keys(t, 64, [&](int kk, uint32_t, uint32_t cd) {
+                if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
                 for (int i = 0; i < nd; ++i) {
                     const int p = d.dl[i], dp = dep[p];
                     if (((cd ^ code[p]) >> (2 * (D - dp))) == 0u) {
@@ -1501,7 +1492,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
                         break;
                     }
                 }
-            }
+            });
             wsync();
             for (int i = t; i < nd; i += 64) atomicAnd(&d.bins[L_code()[d.dl[i]] >> bsh], ~kObDeep);
             wsync();
@@ -1737,31 +1728,17 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
         for (int i = t; i < nd; i += kObThreads) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
         __syncthreads();
     }
-    for (int k0 = t; nd > 0 && k0 < K; k0 += kObThreads * kObBatch) {  // the first sweep's keys: the thread's own writes
-        uint32_t cd[kObBatch], rs[kObBatch];
-#pragma unroll
-        for (int u = 0; u < kObBatch; ++u) {
-            const int k = k0 + kObThreads * u;
-            cd[u] = k < K ? kcode[k] : 0u;
-            rs[u] = k < K ? kresp[k] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kObBatch; ++u) {
-            const int k = k0 + kObThreads * u;
-            if (k >= K) continue;
-            uint32_t p = 0xFFFFFFFFu;
-            if (d.bins[cd[u] >> bsh] == kObDeep) {
-                for (int i = 0; i < nd; ++i) {
-                    const int q = d.dl[i];
-                    if (((cd[u] ^ code[q]) >> (2 * (D - dep[q]))) == 0u) {
-                        p = (uint32_t)q;
-                        break;
-                    }
+    if (nd > 0)
+        for_keys(t, kObThreads, [&](int kk, uint32_t v, uint32_t cd) {
+            if (kk >= K || d.bins[cd >> bsh] != kObDeep) return;
+            for (int i = 0; i < nd; ++i) {
+                const int q = d.dl[i];
+                if (((cd ^ code[q]) >> (2 * (D - dep[q]))) == 0u) {
+                    atomicMax(&best[q], (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)kk));
+                    break;
                 }
             }
-            if (p < (uint32_t)S) atomicMax(&best[p], (rs[u] << 24) | (0xFFFFFFu - (uint32_t)k));
-        }
-    }
+        });
     __syncthreads();
     for (int p = t; p < S; p += kObThreads) {
         const uint32_t bv = best[p];
@@ -2690,7 +2667,7 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(k_octree_bins, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells, cell_count, slots,
-                           octab, kd, kn, lvl_kp, lvl_count, overflow, maxcell, prof);
+                           octab, lvl_kp, lvl_count, overflow, maxcell, prof);
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
