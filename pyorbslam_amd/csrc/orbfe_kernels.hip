@@ -503,7 +503,18 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         const float rq = __builtin_amdgcn_rcpf((float)qrow);
         auto div_q = [&](int n) { return (int)__builtin_fmaf((float)n, rq, 0.5f * rq); };
         const int step_y = div_q(64), step_x = 64 - step_y * qrow;
-        int npq = 0;
+        // Two queues when minTh < iniTh (ORBextractor.cpp:795-815: FAST at iniTh, then minTh only for a
+        // cell where iniTh found nothing): B = pairs whose bound exceeds minTh (from the front of pq), and
+        // its subset A = bound above iniTh (from the back, growing down).  Exact M, NMS and output run on A
+        // first; B is processed only for a cell that A leaves empty.  A pixel outside every A pair has
+        // M <= bound <= iniTh, so it can neither be an iniTh corner nor beat one in the NMS: the iniTh pass
+        // needs M of the A pairs only.  Should the two queues meet (a cell where more than half of the pairs
+        // pass at minTh), the cell takes the one-pass path below instead (both thresholds over B).
+        const bool two = g.min_th < g.ini_th;
+        const int tA = g.ini_th;
+        const int cap = g.fd_pq;
+        int npq = 0, npa = 0;
+        bool collide = false;
         {
             // two 64-quad steps per iteration: both steps' ROI reads are issued before either waits
             // (one LDS round trip per 128 quads); lanes past the window read a clamped row and vote 0
@@ -516,29 +527,43 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     ++y;
                 }
             };
-            auto bound = [&](int i, int y, int x4, bool& ca, bool& cb) {
+            auto bound = [&](int i, int y, int x4, bool& ca, bool& cb, bool& aa, bool& ab) {
                 fd_s2 ba, bb;
                 fast_bound_quad<S>((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4), ba, bb);
                 const bool in = i < nquad;
-                ca = in & ((ba.x > tq) | ((ba.y > tq) & (x4 + 1 < ww)));
-                cb = in & (x4 + 2 < ww) & ((bb.x > tq) | ((bb.y > tq) & (x4 + 3 < ww)));
+                const bool va = x4 + 1 < ww, vb2 = x4 + 2 < ww, vb3 = x4 + 3 < ww;
+                ca = in & ((ba.x > tq) | ((ba.y > tq) & va));
+                cb = in & vb2 & ((bb.x > tq) | ((bb.y > tq) & vb3));
+                aa = ca & ((ba.x > tA) | ((ba.y > tA) & va));
+                ab = cb & ((bb.x > tA) | ((bb.y > tA) & vb3));
             };
-            auto emit = [&](int y, int x4, bool ca, bool cb) {
+            auto emit = [&](int y, int x4, bool ca, bool cb, bool aa, bool ab) {
                 const uint64_t b0 = __ballot(ca), b1 = __ballot(cb);
                 const int o = npq + lanes_below(b0) + lanes_below(b1);
                 const uint16_t e = (uint16_t)((y << 6) | x4);
                 if (ca) pq[o] = e;
                 if (cb) pq[o + (int)ca] = (uint16_t)(e + 2);
                 npq += __popcll(b0) + __popcll(b1);
+                if (two) {
+                    const uint64_t a0 = __ballot(aa), a1 = __ballot(ab);
+                    const int na = __popcll(a0) + __popcll(a1);
+                    collide |= npq + npa + na > cap;
+                    if (!collide) {
+                        const int oa = npa + lanes_below(a0) + lanes_below(a1);
+                        if (aa) pq[cap - 1 - oa] = e;
+                        if (ab) pq[cap - 1 - oa - (int)aa] = (uint16_t)(e + 2);
+                    }
+                    npa += na;
+                }
             };
             for (int i0 = 0; i0 < nquad; i0 += 128) {
                 int qy2 = qy, qx2 = qx;
                 advance(qy2, qx2);
-                bool ca0, cb0, ca1, cb1;
-                bound(i0 + lane, qy, 4 * qx, ca0, cb0);
-                bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1);
-                emit(qy, 4 * qx, ca0, cb0);
-                emit(qy2, 4 * qx2, ca1, cb1);
+                bool ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
+                bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
+                bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
+                emit(qy, 4 * qx, ca0, cb0, aa0, ab0);
+                emit(qy2, 4 * qx2, ca1, cb1, aa1, ab1);
                 qy = qy2;
                 qx = qx2;
                 advance(qy, qx);
@@ -549,89 +574,117 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = npq & 0;
             return;
         }
-        // ---- 3. exact M of the queued pairs -> M map; NMS candidates -> queue
-        const int tlow = max(tq, 1);
-        int nnq = 0;
-        // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
-        uint32_t e_next = lane < npq ? pq[lane] : 0u;
-        for (int k0 = 0; k0 < npq; k0 += 64) {
-            bool h0 = false, h1 = false;
-            const uint32_t e = e_next;
-            if (k0 + 64 + lane < npq) e_next = pq[k0 + 64 + lane];
-            if (k0 + lane < npq) {
-                const int x = e & 63, y = e >> 6;
-                // odd width: the last pair's second pixel lies outside the window; its map entry is cleared
-                // after this stage
-                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
-                // the u8 map keeps M itself (low byte of each biased half)
-                *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
-                h0 = (int)(m & 0x3FFu) > tlow;
-                h1 = (int)((m >> 16) & 0x3FFu) > tlow;
+        // ---- 3. exact M of a queue's pairs -> M map; the pairs with a pixel above tl are compacted in place
+        //         (entry i at qb[dir * i]: dir -1 for A at the back of pq) into the NMS queue; returns its length
+        auto m_stage = [&](uint16_t* qb, int dir, int n, int tl) {
+            int nn = 0;
+            // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
+            uint32_t e_next = lane < n ? qb[dir * lane] : 0u;
+            for (int k0 = 0; k0 < n; k0 += 64) {
+                bool h0 = false, h1 = false;
+                const uint32_t e = e_next;
+                if (k0 + 64 + lane < n) e_next = qb[dir * (k0 + 64 + lane)];
+                if (k0 + lane < n) {
+                    const int x = e & 63, y = e >> 6;
+                    // odd width: the last pair's second pixel lies outside the window; its map entry is cleared
+                    // after this stage
+                    const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
+                    // the u8 map keeps M itself (low byte of each biased half)
+                    *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
+                    h0 = (int)(m & 0x3FFu) > tl;
+                    h1 = (int)((m >> 16) & 0x3FFu) > tl;
+                }
+                // slots below k0 + 64 are written; every read of the queue (this step's entries, the next
+                // step's prefetch) was issued before
+                const bool h = h0 | h1;
+                const uint64_t bh = __ballot(h);
+                if (h) qb[dir * (nn + lanes_below(bh))] = (uint16_t)e;
+                nn += __popcll(bh);
             }
-            // pairs with a pixel above tlow are compacted in place: slots < k0 + 64 are written, every read of
-            // the queue (this step's entries, the next step's prefetch) was issued before
-            const bool h = h0 | h1;
-            const uint64_t bh = __ballot(h);
-            if (h) pq[nnq + lanes_below(bh)] = (uint16_t)e;
-            nnq += __popcll(bh);
-        }
-        // odd width: column ww (right of the window) got the outside pixel's M from the last pairs; NMS
-        // reads it as a neighbour (and as that pixel's own score) and needs 0 there
-        if ((ww & 1) && lane < wh) mm[(lane + 1) * MP + ww + 2] = 0;
-        __syncthreads();
-        if (V == 3) {  // ablation: + exact M
-            if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
-            return;
-        }
-        // ---- 4. NMS (local max) over the queued pairs + ordered compaction, both thresholds in one pass:
-        //         the neighbour maximum does not depend on t, so each pixel is tested at iniTh and minTh
-        //         together (own > max(neighbours, th) also implies own > tlow).  iniTh survivors go straight
-        //         out; minTh survivors are staged in the (dead) ROI area and copied out only if iniTh kept
-        //         nothing (ORBextractor.cpp:811-815).  Output order: pairs row-major, pixel x before x + 1.
+            // odd width: column ww (right of the window) got the outside pixel's M from the last pairs; NMS
+            // reads it as a neighbour (and as that pixel's own score) and needs 0 there
+            if ((ww & 1) && lane < wh) mm[(lane + 1) * MP + ww + 2] = 0;
+            __syncthreads();
+            return nn;
+        };
+        // ---- 4. NMS (local max) over an NMS queue + ordered compaction.  For t >= 1, "score > every
+        //         8-neighbour's score at t" is M > t and M > max(neighbour M) (a neighbour with M <= t is
+        //         below anyway).  Kept pixels: pairs row-major, pixel x before x + 1 = cv::FAST's order.
+        //         thb1 >= 1: also test the second threshold and stage its survivors in `alt` (one-pass path).
         uint32_t* out = slots + (int64_t)img * g.slot_total + cg.slot_off;
         uint32_t* alt = (uint32_t*)roi;  // >= 2 * slot_cap u16 (detect_roi_elems)
-        const bool fb = g.min_th != g.ini_th;
-        const int thb0 = max(g.ini_th, 1), thb1 = max(g.min_th, 1);
-        int t0 = 0, t1 = 0;
-        for (int k0 = 0; k0 < nnq; k0 += 64) {
-            bool ka0 = false, kb0 = false, ka1 = false, kb1 = false;
-            uint32_t reca = 0, recb = 0;
-            if (k0 + lane < nnq) {
-                const int e = pq[k0 + lane];
-                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
-                const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
-                const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
-                const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
-                const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
-                const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
-                const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
-                ka0 = owna > max(na, thb0);
-                ka1 = owna > max(na, thb1);
-                kb0 = ownb > max(nb, thb0);
-                kb1 = ownb > max(nb, thb1);
-                const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
-                reca = xy | ((uint32_t)(owna - 1) << 24);
-                recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
+        auto nms_stage = [&](const uint16_t* qb, int dir, int nn, int thb0, int thb1, int& t0, int& t1) {
+            t0 = t1 = 0;
+            for (int k0 = 0; k0 < nn; k0 += 64) {
+                bool ka0 = false, kb0 = false, ka1 = false, kb1 = false;
+                uint32_t reca = 0, recb = 0;
+                if (k0 + lane < nn) {
+                    const int e = qb[dir * (k0 + lane)];
+                    const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
+                    const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
+                    const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
+                    const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
+                    const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
+                    const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
+                    const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
+                    ka0 = owna > max(na, thb0);
+                    kb0 = ownb > max(nb, thb0);
+                    if (thb1 > 0) {
+                        ka1 = owna > max(na, thb1);
+                        kb1 = ownb > max(nb, thb1);
+                    }
+                    const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
+                    reca = xy | ((uint32_t)(owna - 1) << 24);
+                    recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
+                }
+                const uint64_t ba0 = __ballot(ka0), bb0 = __ballot(kb0);
+                const int o0 = t0 + lanes_below(ba0) + lanes_below(bb0);
+                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+                if (ka0 && o0 < cg.slot_cap) out[o0] = reca;
+                if (kb0 && o0 + (int)ka0 < cg.slot_cap) out[o0 + (int)ka0] = recb;
+                t0 += __popcll(ba0) + __popcll(bb0);
+                if (thb1 > 0) {
+                    const uint64_t ba1 = __ballot(ka1), bb1 = __ballot(kb1);
+                    const int o1 = t1 + lanes_below(ba1) + lanes_below(bb1);
+                    if (ka1 && o1 < cg.slot_cap) alt[o1] = reca;
+                    if (kb1 && o1 + (int)ka1 < cg.slot_cap) alt[o1 + (int)ka1] = recb;
+                    t1 += __popcll(ba1) + __popcll(bb1);
+                }
             }
-            const uint64_t ba0 = __ballot(ka0), bb0 = __ballot(kb0);
-            const int o0 = t0 + lanes_below(ba0) + lanes_below(bb0);
-            // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-            if (ka0 && o0 < cg.slot_cap) out[o0] = reca;
-            if (kb0 && o0 + (int)ka0 < cg.slot_cap) out[o0 + (int)ka0] = recb;
-            t0 += __popcll(ba0) + __popcll(bb0);
-            if (fb) {
-                const uint64_t ba1 = __ballot(ka1), bb1 = __ballot(kb1);
-                const int o1 = t1 + lanes_below(ba1) + lanes_below(bb1);
-                if (ka1 && o1 < cg.slot_cap) alt[o1] = reca;
-                if (kb1 && o1 + (int)ka1 < cg.slot_cap) alt[o1 + (int)ka1] = recb;
-                t1 += __popcll(ba1) + __popcll(bb1);
+        };
+        int total = 0;
+        if (two && !collide) {
+            int t0, t1;
+            const int nna = m_stage(pq + cap - 1, -1, npa, max(tA, 1));
+            if (V == 3) {  // ablation: + exact M
+                if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nna & 0;
+                return;
             }
-        }
-        int total = t0;
-        if (t0 == 0 && t1 > 0) {
-            __syncthreads();
-            for (int i = lane; i < min(t1, cg.slot_cap); i += 64) out[i] = alt[i];
-            total = t1;
+            nms_stage(pq + cap - 1, -1, nna, max(g.ini_th, 1), 0, t0, t1);
+            total = t0;
+            if (t0 == 0) {  // minTh fallback: every pair of B (the A pairs' M is recomputed, identically)
+                const int nnb = m_stage(pq, 1, npq, max(g.min_th, 1));
+                nms_stage(pq, 1, nnb, max(g.min_th, 1), 0, t0, t1);
+                total = t0;
+            }
+        } else {
+            // one pass over B at tq = min(iniTh, minTh), both thresholds in the NMS: iniTh survivors go
+            // straight out, minTh survivors are staged in the (dead) ROI area and copied out only if iniTh
+            // kept nothing
+            const int nnq = m_stage(pq, 1, npq, max(tq, 1));
+            if (V == 3) {  // ablation: + exact M
+                if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = nnq & 0;
+                return;
+            }
+            const bool fb = g.min_th != g.ini_th;
+            int t0, t1;
+            nms_stage(pq, 1, nnq, max(g.ini_th, 1), fb ? max(g.min_th, 1) : 0, t0, t1);
+            total = t0;
+            if (t0 == 0 && t1 > 0) {
+                __syncthreads();
+                for (int i = lane; i < min(t1, cg.slot_cap); i += 64) out[i] = alt[i];
+                total = t1;
+            }
         }
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
         };
