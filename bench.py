@@ -628,7 +628,7 @@ def main():
 
     c3 = None
     if extras and world == 1 and not args.no_c3 and (ROOT / "tests" / "golden" / "sequence_kitti_synth.npz").exists():
-        c3 = run_c3(32, 1)
+        c3 = run_c3(0, 1)
         if not c3["parity_ok"]:
             print(json.dumps({"error": "C3 tracking-loop parity failure", "details": c3["parity"]}), flush=True)
             raise SystemExit(3)

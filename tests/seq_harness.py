@@ -32,7 +32,7 @@ from pathlib import Path
 import numpy as np
 
 GOLDEN_FILE = Path(__file__).resolve().parent / "golden" / "sequence_kitti_synth.npz"
-SEQ = dict(seed=0, n_frames=32, width=1241, height=376, speed=0.6)
+SEQ = dict(seed=0, n_frames=96, width=1241, height=376, speed=0.6)
 PARAMS = dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)
 LOCAL_WINDOW = 2      # local map = the map points of the last LOCAL_WINDOW frames (update_local_points)
 GRID_ROWS, GRID_COLS = 48, 64   # Tracking.py:97-98

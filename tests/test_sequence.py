@@ -5,7 +5,7 @@ and both searches' assignments and counts must be identical in every frame.
 
   CPU: the golden's shape, and the first frames replayed through the oracle (extractor restatement,
        stereo restatement, matcher restatement), which pins the harness's own restated pieces.
-  GPU: all 32 frames through the drop-in path — pyORBExtractor.ORBextractor with the pair-batched
+  GPU: all 96 frames through the drop-in path — pyORBExtractor.ORBextractor with the pair-batched
        Frame.ExtractORB, compute_stereo_matches and Frame.copy installed by pyorbslam_amd.frame.install on
        the restated Frame class, and matcher.ORBMatcher."""
 import json
