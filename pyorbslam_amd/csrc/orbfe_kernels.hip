@@ -2130,9 +2130,17 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
         wave_sync_lds();  // hb complete
         // ---- steered BRIEF with the vertical taps per sample: sample (row, col) is blurred row o = row + 18
-        //      (H rows o .. o + 6), column c = col + 21; rint by the 1.5 * 2^23 trick (low mantissa bits
-        //      hold 0x400000 + rint(x))
-        const uint32_t cbase = 21u - __float_as_uint(12582912.0f);
+        //      (H rows o .. o + 6), column c = col + 21.  rint by the 1.5 * 2^23 trick: the f32 bits are
+        //      xb = 0x4B400000 + R with R = rint(row) in [-18, 18], so the row pair m = o >> 1 =
+        //      floor(R / 2) + 9 is (xb >> 1) - 0x25A00000, and the byte address of H pair (m, c) is one
+        //      v_mad_u32_u24 (which reads the low 24 bits of xb >> 1, 0xA00000 + floor(R / 2)) over one
+        //      v_lshl_add of the column bits; the constants fold into kc.  The 4 dwords P[m .. m + 3] hold
+        //      rows 2m .. 2m + 7: for even o the taps are their low / high halves in order, for odd o every
+        //      tap sits one u16 higher, so the data is shifted by 16 * (R & 1) bits (v_alignbit takes bits
+        //      4:0 of xb << 4) and the weights stay fixed.  The last dword's high half has weight 0.
+        typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+        const uint32_t kc = (uint32_t)(uintptr_t)(lds_u32*)hb + (uint32_t)(4 * (9 * kHDw + 21)) -
+                            (uint32_t)(4 * kHDw) * 0xA00000u - (__float_as_uint(12582912.0f) << 2);
         uint32_t mine_lo = 0, mine_hi = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
 #pragma unroll 1
         for (int i = 0; i < 4; ++i) {
@@ -2143,16 +2151,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 const float px = e ? pt.z : pt.x, py = e ? pt.w : pt.y;
                 const df2 mm = (df2){py, py} * (df2){a, -b};
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
-                const uint32_t o = (__float_as_uint(rc.x) & 0xFFFFFFu) - 0x400000u + 18u;
-                // c < 64: the mask lets the compiler put the four row offsets into the ds_read offsets
-                const uint32_t c = (__float_as_uint(rc.y) + cbase) & 63u;
-                const uint32_t* p = hb + (o >> 1) * kHDw + c;
+                const uint32_t xb = __float_as_uint(rc.x), yb = __float_as_uint(rc.y);
+                const uint32_t addr = ((xb >> 1) & 0xFFFFFFu) * (uint32_t)(4 * kHDw) + ((yb << 2) + kc);
+                lds_u32* p = (lds_u32*)(uintptr_t)addr;
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
-                const bool odd = o & 1u;
-                uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), odd ? w2(0, 18) : w2(18, 34), 32768u, false);
-                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), odd ? w2(34, 48) : w2(48, 56), s, false);
-                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), odd ? w2(56, 48) : w2(48, 34), s, false);
-                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), odd ? w2(34, 18) : w2(18, 0), s, false);
+                const uint32_t sh = xb << 4;
+                uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p1, p0, sh)), w2(18, 34), 32768u, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p2, p1, sh)), w2(48, 56), s, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p3, p2, sh)), w2(48, 34), s, false);
+                s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3 >> (sh & 31u)), w2(18, 0), s, false);
                 v2[e] = s >> 16;
             }
             const uint64_t bb = __ballot(v2[0] < v2[1]);
