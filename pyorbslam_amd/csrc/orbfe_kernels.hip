@@ -2153,8 +2153,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
                 const uint32_t xb = __float_as_uint(rc.x), yb = __float_as_uint(rc.y);
                 const uint32_t addr = ((xb >> 1) & 0xFFFFFFu) * (uint32_t)(4 * kHDw) + ((yb << 2) + kc);
+#if defined(ORBFE_X_NOCONF)  // experiment (tools/dbg/build_variant.sh): conflict-free reads, wrong bits
+                lds_u32* p = (lds_u32*)(uintptr_t)((uint32_t)(uintptr_t)(lds_u32*)hb + 4 * (lane & 31) + (addr & 0x40));
+                const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
+#elif defined(ORBFE_X_NOBRIEFLDS)  // experiment: no BRIEF LDS reads at all, wrong bits
+                const uint32_t p0 = addr, p1 = addr ^ xb, p2 = addr + yb, p3 = xb ^ yb;
+#else
                 lds_u32* p = (lds_u32*)(uintptr_t)addr;
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
+#endif
                 const uint32_t sh = xb << 4;
                 uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p1, p0, sh)), w2(18, 34), 32768u, false);
                 s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p2, p1, sh)), w2(48, 56), s, false);
@@ -2164,7 +2171,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             }
             const uint64_t bb = __ballot(v2[0] < v2[1]);
             // lane i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
-            // 3-5 % slower, profiles/r02/ab_r2p.log, ab_r2q.log)
+            // 3-5 % slower in round 2)
             mine_lo = writelane_m0(mine_lo, (uint32_t)bb, i);
             mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), i);
         }
