@@ -527,25 +527,32 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     ++y;
                 }
             };
-            auto bound = [&](int i, int y, int x4, bool& ca, bool& cb, bool& aa, bool& ab) {
+            // the pass conditions as lane masks (v_cmp straight into SGPR pairs, combined on the SALU): a
+            // bool per lane would cost a v_cndmask + v_cmp round trip per ballot.  Only the last quad of a
+            // row can hold pixels past the window (x4 == xl); rem = ww - xl of its 4 are inside.
+            const int xl = 4 * (qrow - 1), rem = ww - xl;
+            auto gt = [](int a, int b) { return (uint64_t)__builtin_amdgcn_sicmp(a, b, 38); };  // ICMP_SGT
+            auto bound = [&](int i, int y, int x4, uint64_t& ca, uint64_t& cb, uint64_t& aa, uint64_t& ab) {
                 fd_s2 ba, bb;
                 fast_bound_quad<S>((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4), ba, bb);
-                const bool in = i < nquad;
-                const bool va = x4 + 1 < ww, vb2 = x4 + 2 < ww, vb3 = x4 + 3 < ww;
-                ca = in & ((ba.x > tq) | ((ba.y > tq) & va));
-                cb = in & vb2 & ((bb.x > tq) | ((bb.y > tq) & vb3));
-                aa = ca & ((ba.x > tA) | ((ba.y > tA) & va));
-                ab = cb & ((bb.x > tA) | ((bb.y > tA) & vb3));
+                const uint64_t in = __builtin_amdgcn_sicmp(i, nquad, 40);  // ICMP_SLT
+                const uint64_t last = __builtin_amdgcn_sicmp(x4, xl, 32);  // ICMP_EQ
+                const uint64_t va = rem > 1 ? ~0ull : ~last, vb2 = rem > 2 ? ~0ull : ~last,
+                               vb3 = rem > 3 ? ~0ull : ~last;
+                ca = in & (gt(ba.x, tq) | (gt(ba.y, tq) & va));
+                cb = in & vb2 & (gt(bb.x, tq) | (gt(bb.y, tq) & vb3));
+                aa = ca & (gt(ba.x, tA) | (gt(ba.y, tA) & va));
+                ab = cb & (gt(bb.x, tA) | (gt(bb.y, tA) & vb3));
             };
-            auto emit = [&](int y, int x4, bool ca, bool cb, bool aa, bool ab) {
-                const uint64_t b0 = __ballot(ca), b1 = __ballot(cb);
+            auto emit = [&](int y, int x4, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
+                const bool ca = __builtin_amdgcn_inverse_ballot_w64(b0), cb = __builtin_amdgcn_inverse_ballot_w64(b1);
                 const int o = npq + lanes_below(b0) + lanes_below(b1);
                 const uint16_t e = (uint16_t)((y << 6) | x4);
                 if (ca) pq[o] = e;
                 if (cb) pq[o + (int)ca] = (uint16_t)(e + 2);
                 npq += __popcll(b0) + __popcll(b1);
                 if (two) {
-                    const uint64_t a0 = __ballot(aa), a1 = __ballot(ab);
+                    const bool aa = __builtin_amdgcn_inverse_ballot_w64(a0), ab = __builtin_amdgcn_inverse_ballot_w64(a1);
                     const int na = __popcll(a0) + __popcll(a1);
                     collide |= npq + npa + na > cap;
                     if (!collide) {
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             for (int i0 = 0; i0 < nquad; i0 += 128) {
                 int qy2 = qy, qx2 = qx;
                 advance(qy2, qx2);
-                bool ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
+                uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
                 bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
                 bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
                 emit(qy, 4 * qx, ca0, cb0, aa0, ab0);
@@ -581,24 +588,22 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
             uint32_t e_next = lane < n ? qb[dir * lane] : 0u;
             for (int k0 = 0; k0 < n; k0 += 64) {
-                bool h0 = false, h1 = false;
+                // every lane computes (a lane past n repeats an earlier entry of its own, harmlessly); the map
+                // store and the compaction take the lanes of this step's entries (lane masks, as the pre-test)
                 const uint32_t e = e_next;
                 if (k0 + 64 + lane < n) e_next = qb[dir * (k0 + 64 + lane)];
-                if (k0 + lane < n) {
-                    const int x = e & 63, y = e >> 6;
-                    // odd width: the last pair's second pixel lies outside the window; its map entry is cleared
-                    // after this stage
-                    const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
-                    // the u8 map keeps M itself (low byte of each biased half)
+                const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, n, 40);  // ICMP_SLT
+                const int x = e & 63, y = e >> 6;
+                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
+                // the u8 map keeps M itself (low byte of each biased half); odd width: the last pair's second
+                // pixel lies outside the window, its map entry is cleared after this stage
+                if (__builtin_amdgcn_inverse_ballot_w64(inr))
                     *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
-                    h0 = (int)(m & 0x3FFu) > tl;
-                    h1 = (int)((m >> 16) & 0x3FFu) > tl;
-                }
                 // slots below k0 + 64 are written; every read of the queue (this step's entries, the next
                 // step's prefetch) was issued before
-                const bool h = h0 | h1;
-                const uint64_t bh = __ballot(h);
-                if (h) qb[dir * (nn + lanes_below(bh))] = (uint16_t)e;
+                const uint64_t bh = inr & ((uint64_t)__builtin_amdgcn_sicmp((int)(m & 0x3FFu), tl, 38) |
+                                           (uint64_t)__builtin_amdgcn_sicmp((int)((m >> 16) & 0x3FFu), tl, 38));
+                if (__builtin_amdgcn_inverse_ballot_w64(bh)) qb[dir * (nn + lanes_below(bh))] = (uint16_t)e;
                 nn += __popcll(bh);
             }
             // odd width: column ww (right of the window) got the outside pixel's M from the last pairs; NMS
@@ -616,40 +621,32 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         auto nms_stage = [&](const uint16_t* qb, int dir, int nn, int thb0, int thb1, int& t0, int& t1) {
             t0 = t1 = 0;
             for (int k0 = 0; k0 < nn; k0 += 64) {
-                bool ka0 = false, kb0 = false, ka1 = false, kb1 = false;
-                uint32_t reca = 0, recb = 0;
-                if (k0 + lane < nn) {
-                    const int e = qb[dir * (k0 + lane)];
-                    const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
-                    const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
-                    const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
-                    const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
-                    const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
-                    const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
-                    const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
-                    ka0 = owna > max(na, thb0);
-                    kb0 = ownb > max(nb, thb0);
-                    if (thb1 > 0) {
-                        ka1 = owna > max(na, thb1);
-                        kb1 = ownb > max(nb, thb1);
-                    }
-                    const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
-                    reca = xy | ((uint32_t)(owna - 1) << 24);
-                    recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
-                }
-                const uint64_t ba0 = __ballot(ka0), bb0 = __ballot(kb0);
-                const int o0 = t0 + lanes_below(ba0) + lanes_below(bb0);
-                // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
-                if (ka0 && o0 < cg.slot_cap) out[o0] = reca;
-                if (kb0 && o0 + (int)ka0 < cg.slot_cap) out[o0 + (int)ka0] = recb;
-                t0 += __popcll(ba0) + __popcll(bb0);
-                if (thb1 > 0) {
-                    const uint64_t ba1 = __ballot(ka1), bb1 = __ballot(kb1);
-                    const int o1 = t1 + lanes_below(ba1) + lanes_below(bb1);
-                    if (ka1 && o1 < cg.slot_cap) alt[o1] = reca;
-                    if (kb1 && o1 + (int)ka1 < cg.slot_cap) alt[o1 + (int)ka1] = recb;
-                    t1 += __popcll(ba1) + __popcll(bb1);
-                }
+                // every lane computes on an entry in range; lane masks select the kept pixels
+                const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, nn, 40);  // ICMP_SLT
+                const int e = qb[dir * min(k0 + lane, nn - 1)];
+                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
+                const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
+                const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
+                const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
+                const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
+                const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
+                const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
+                const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
+                const uint32_t reca = xy | ((uint32_t)(owna - 1) << 24);
+                const uint32_t recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
+                auto keep = [&](int th, uint64_t& ba, uint64_t& bb, int& t, uint32_t* dst) {
+                    ba = inr & (uint64_t)__builtin_amdgcn_sicmp(owna, max(na, th), 38);
+                    bb = inr & (uint64_t)__builtin_amdgcn_sicmp(ownb, max(nb, th), 38);
+                    const bool ka = __builtin_amdgcn_inverse_ballot_w64(ba), kb = __builtin_amdgcn_inverse_ballot_w64(bb);
+                    const int o = t + lanes_below(ba) + lanes_below(bb);
+                    // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
+                    if (ka && o < cg.slot_cap) dst[o] = reca;
+                    if (kb && o + (int)ka < cg.slot_cap) dst[o + (int)ka] = recb;
+                    t += __popcll(ba) + __popcll(bb);
+                };
+                uint64_t ba, bb;
+                keep(thb0, ba, bb, t0, out);
+                if (thb1 > 0) keep(thb1, ba, bb, t1, alt);
             }
         };
         int total = 0;
