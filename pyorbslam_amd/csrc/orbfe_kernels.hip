@@ -532,17 +532,20 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             // row can hold pixels past the window (x4 == xl); rem = ww - xl of its 4 are inside.
             const int xl = 4 * (qrow - 1), rem = ww - xl;
             auto gt = [](int a, int b) { return (uint64_t)__builtin_amdgcn_sicmp(a, b, 38); };  // ICMP_SGT
-            auto bound = [&](int i, int y, int x4, uint64_t& ca, uint64_t& cb, uint64_t& aa, uint64_t& ab) {
+            auto bound_at = [&](const uint32_t* R, uint64_t in, uint64_t last, uint64_t& ca, uint64_t& cb, uint64_t& aa,
+                                uint64_t& ab) {
                 fd_s2 ba, bb;
-                fast_bound_quad<S>((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4), ba, bb);
-                const uint64_t in = __builtin_amdgcn_sicmp(i, nquad, 40);  // ICMP_SLT
-                const uint64_t last = __builtin_amdgcn_sicmp(x4, xl, 32);  // ICMP_EQ
+                fast_bound_quad<S>(R, ba, bb);
                 const uint64_t va = rem > 1 ? ~0ull : ~last, vb2 = rem > 2 ? ~0ull : ~last,
                                vb3 = rem > 3 ? ~0ull : ~last;
                 ca = in & (gt(ba.x, tq) | (gt(ba.y, tq) & va));
                 cb = in & vb2 & (gt(bb.x, tq) | (gt(bb.y, tq) & vb3));
                 aa = ca & (gt(ba.x, tA) | (gt(ba.y, tA) & va));
                 ab = cb & (gt(bb.x, tA) | (gt(bb.y, tA) & vb3));
+            };
+            auto bound = [&](int i, int y, int x4, uint64_t& ca, uint64_t& cb, uint64_t& aa, uint64_t& ab) {
+                bound_at((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4),
+                         __builtin_amdgcn_sicmp(i, nquad, 40), __builtin_amdgcn_sicmp(x4, xl, 32), ca, cb, aa, ab);
             };
             auto emit = [&](int y, int x4, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
                 const bool ca = __builtin_amdgcn_inverse_ballot_w64(b0), cb = __builtin_amdgcn_inverse_ballot_w64(b1);
@@ -563,17 +566,36 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     npa += na;
                 }
             };
-            for (int i0 = 0; i0 < nquad; i0 += 128) {
-                int qy2 = qy, qx2 = qx;
-                advance(qy2, qx2);
-                uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
-                bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
-                bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
-                emit(qy, 4 * qx, ca0, cb0, aa0, ab0);
-                emit(qy2, 4 * qx2, ca1, cb1, aa1, ab1);
-                qy = qy2;
-                qx = qx2;
-                advance(qy, qx);
+            if (qrow <= 8) {
+                // rows of 8 lanes (every KITTI / EuRoC cell but EuRoC level 7's): lane 8 r + qx takes quad qx
+                // of row y0 + r (lanes qx >= qrow idle), so the lane order is the row-major queue order and
+                // the ROI address and the entry are per-lane constants plus a uniform row offset.  Lanes of
+                // rows past the window read (and vote 0 on) rows below it: still inside the LDS allocation
+                // (ROI rows, then the M map).
+                const int r = lane >> 3, qx = lane & 7;
+                const uint64_t colok = __builtin_amdgcn_sicmp(qx, qrow, 40), last = __builtin_amdgcn_sicmp(4 * qx, xl, 32);
+                const uint32_t* R0 = (const uint32_t*)(roi + (r + 3) * RP + 4 * qx + 4);
+                for (int y0 = 0; y0 < wh; y0 += 16) {
+                    uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
+                    bound_at(R0 + y0 * S, colok & __builtin_amdgcn_sicmp(r, wh - y0, 40), last, ca0, cb0, aa0, ab0);
+                    bound_at(R0 + (y0 + 8) * S, colok & __builtin_amdgcn_sicmp(r, wh - y0 - 8, 40), last, ca1, cb1, aa1,
+                             ab1);
+                    emit(y0 + r, 4 * qx, ca0, cb0, aa0, ab0);
+                    emit(y0 + 8 + r, 4 * qx, ca1, cb1, aa1, ab1);
+                }
+            } else {
+                for (int i0 = 0; i0 < nquad; i0 += 128) {
+                    int qy2 = qy, qx2 = qx;
+                    advance(qy2, qx2);
+                    uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
+                    bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
+                    bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
+                    emit(qy, 4 * qx, ca0, cb0, aa0, ab0);
+                    emit(qy2, 4 * qx2, ca1, cb1, aa1, ab1);
+                    qy = qy2;
+                    qx = qx2;
+                    advance(qy, qx);
+                }
             }
         }
         __syncthreads();
