@@ -514,7 +514,6 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         const int tA = g.ini_th;
         const int cap = g.fd_pq;
         int npq = 0, npa = 0;
-        bool collide = false;
         {
             // two 64-quad steps per iteration: both steps' ROI reads are issued before either waits
             // (one LDS round trip per 128 quads); lanes past the window read a clamped row and vote 0
@@ -547,21 +546,32 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 bound_at((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4),
                          __builtin_amdgcn_sicmp(i, nquad, 40), __builtin_amdgcn_sicmp(x4, xl, 32), ca, cb, aa, ab);
             };
+            // a lane's second entry goes after its first: its offset counts the first-entry bits at or below
+            // the lane, mbcnt(b0 >> 1) + bit 0 of b0 (uniform), on top of the second-entry bits below it
             auto emit = [&](int y, int x4, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
                 const bool ca = __builtin_amdgcn_inverse_ballot_w64(b0), cb = __builtin_amdgcn_inverse_ballot_w64(b1);
-                const int o = npq + lanes_below(b0) + lanes_below(b1);
+                const int n1 = lanes_below(b1);
                 const uint16_t e = (uint16_t)((y << 6) | x4);
-                if (ca) pq[o] = e;
-                if (cb) pq[o + (int)ca] = (uint16_t)(e + 2);
+                if (ca) pq[npq + lanes_below(b0) + n1] = e;
+                const uint64_t b0s = b0 >> 1;
+                if (cb)
+                    pq[npq + (int)(b0 & 1) +
+                       (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0s >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0s, n1))] =
+                        (uint16_t)(e + 2);
                 npq += __popcll(b0) + __popcll(b1);
                 if (two) {
                     const bool aa = __builtin_amdgcn_inverse_ballot_w64(a0), ab = __builtin_amdgcn_inverse_ballot_w64(a1);
                     const int na = __popcll(a0) + __popcll(a1);
-                    collide |= npq + npa + na > cap;
-                    if (!collide) {
-                        const int oa = npa + lanes_below(a0) + lanes_below(a1);
-                        if (aa) pq[cap - 1 - oa] = e;
-                        if (ab) pq[cap - 1 - oa - (int)aa] = (uint16_t)(e + 2);
+                    // both counts only grow: once the queues would meet they stay met (collide below), and A
+                    // stops writing so that B stays intact for the one-pass path
+                    if (npq + npa + na <= cap) {
+                        const int m1 = lanes_below(a1);
+                        if (aa) pq[cap - 1 - npa - lanes_below(a0) - m1] = e;
+                        const uint64_t a0s = a0 >> 1;
+                        if (ab)
+                            pq[cap - 1 - npa - (int)(a0 & 1) -
+                               (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(a0s >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0s, m1))] =
+                                (uint16_t)(e + 2);
                     }
                     npa += na;
                 }
@@ -671,6 +681,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 if (thb1 > 0) keep(thb1, ba, bb, t1, alt);
             }
         };
+        const bool collide = npq + npa > cap;
         int total = 0;
         if (two && !collide) {
             int t0, t1;
