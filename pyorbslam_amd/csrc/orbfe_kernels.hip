@@ -416,9 +416,13 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // ROI (max_rh rows x RP u16); after the M stage the same bytes stage the minTh survivors (u32 records)
     uint16_t* roi = (uint16_t*)lds;
-    const int MP = g.fd_mp & 0xFFFF;  // provably 16-bit: row offsets use v_mul_u32_u24
-    uint8_t* mm = (uint8_t*)(roi + detect_roi_elems(g, RP));   // u8 M, (max_wh + 2) x MP: px (x, y) at (y + 1) * MP + x + 2
-    // pair queue (y << 6) | x, x even (fd_pq entries); the M stage compacts it in place into the NMS queue
+    // u8 M map, (max_wh + 2) rows of MP = RP bytes: px (x, y) at (y + 1) * MP + x + 2, i.e. at the pair's queue
+    // entry minus 2 MP + 2
+    constexpr int MP = RP;
+    uint8_t* mm = (uint8_t*)(roi + detect_roi_elems(g, RP));
+    // pair queue: entry = ROI u16 index of the pair's first pixel, (y + 3) * RP + x + 4 (x even; fd_pq
+    // entries), so the M stage's ROI and map addresses are the entry itself; the M stage compacts it in
+    // place into the NMS queue
     uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));
     int bx, img;
     xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
@@ -548,10 +552,10 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             };
             // a lane's second entry goes after its first: its offset counts the first-entry bits at or below
             // the lane, mbcnt(b0 >> 1) + bit 0 of b0 (uniform), on top of the second-entry bits below it
-            auto emit = [&](int y, int x4, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
+            auto emit = [&](int n, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
                 const bool ca = __builtin_amdgcn_inverse_ballot_w64(b0), cb = __builtin_amdgcn_inverse_ballot_w64(b1);
                 const int n1 = lanes_below(b1);
-                const uint16_t e = (uint16_t)((y << 6) | x4);
+                const uint16_t e = (uint16_t)n;
                 if (ca) pq[npq + lanes_below(b0) + n1] = e;
                 const uint64_t b0s = b0 >> 1;
                 if (cb)
@@ -590,8 +594,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     bound_at(R0 + y0 * S, colok & __builtin_amdgcn_sicmp(r, wh - y0, 40), last, ca0, cb0, aa0, ab0);
                     bound_at(R0 + (y0 + 8) * S, colok & __builtin_amdgcn_sicmp(r, wh - y0 - 8, 40), last, ca1, cb1, aa1,
                              ab1);
-                    emit(y0 + r, 4 * qx, ca0, cb0, aa0, ab0);
-                    emit(y0 + 8 + r, 4 * qx, ca1, cb1, aa1, ab1);
+                    emit((y0 + r + 3) * RP + 4 * qx + 4, ca0, cb0, aa0, ab0);
+                    emit((y0 + r + 11) * RP + 4 * qx + 4, ca1, cb1, aa1, ab1);
                 }
             } else {
                 for (int i0 = 0; i0 < nquad; i0 += 128) {
@@ -600,8 +604,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
                     bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
                     bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
-                    emit(qy, 4 * qx, ca0, cb0, aa0, ab0);
-                    emit(qy2, 4 * qx2, ca1, cb1, aa1, ab1);
+                    emit((qy + 3) * RP + 4 * qx + 4, ca0, cb0, aa0, ab0);
+                    emit((qy2 + 3) * RP + 4 * qx2 + 4, ca1, cb1, aa1, ab1);
                     qy = qy2;
                     qx = qx2;
                     advance(qy, qx);
@@ -618,19 +622,18 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         auto m_stage = [&](uint16_t* qb, int dir, int n, int tl) {
             int nn = 0;
             // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
-            uint32_t e_next = lane < n ? qb[dir * lane] : 0u;
+            uint32_t e_next = lane < n ? qb[dir * lane] : (uint32_t)(3 * RP + 4);  // idle lanes: pixel (0, 0)
             for (int k0 = 0; k0 < n; k0 += 64) {
                 // every lane computes (a lane past n repeats an earlier entry of its own, harmlessly); the map
                 // store and the compaction take the lanes of this step's entries (lane masks, as the pre-test)
                 const uint32_t e = e_next;
                 if (k0 + 64 + lane < n) e_next = qb[dir * (k0 + 64 + lane)];
                 const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, n, 40);  // ICMP_SLT
-                const int x = e & 63, y = e >> 6;
-                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + (y + 3) * RP + x + 4));
+                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + e));
                 // the u8 map keeps M itself (low byte of each biased half); odd width: the last pair's second
                 // pixel lies outside the window, its map entry is cleared after this stage
                 if (__builtin_amdgcn_inverse_ballot_w64(inr))
-                    *(uint16_t*)(mm + (y + 1) * MP + x + 2) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
+                    *(uint16_t*)(mm + e - (2 * MP + 2)) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
                 // slots below k0 + 64 are written; every read of the queue (this step's entries, the next
                 // step's prefetch) was issued before
                 const uint64_t bh = inr & ((uint64_t)__builtin_amdgcn_sicmp((int)(m & 0x3FFu), tl, 38) |
@@ -656,14 +659,15 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 // every lane computes on an entry in range; lane masks select the kept pixels
                 const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, nn, 40);  // ICMP_SLT
                 const int e = qb[dir * min(k0 + lane, nn - 1)];
-                const uint8_t* q = mm + ((e >> 6) + 1) * MP + (e & 63) + 2;  // pixel A = (x, y); B = (x + 1, y)
+                const uint8_t* q = mm + e - (2 * MP + 2);  // pixel A = (x, y); B = (x + 1, y)
                 const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
                 const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
                 const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
                 const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
                 const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
                 const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
-                const uint32_t xy = (uint32_t)(cg.x0 + (e & 63) + 3) | ((uint32_t)(cg.y0 + (e >> 6) + 3) << 12);
+                // (x + 3, y + 3) = (e % RP - 1, e / RP)
+                const uint32_t xy = (uint32_t)(cg.x0 + (int)((uint32_t)e % RP) - 1) | ((uint32_t)(cg.y0 + (int)((uint32_t)e / RP)) << 12);
                 const uint32_t reca = xy | ((uint32_t)(owna - 1) << 24);
                 const uint32_t recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
                 auto keep = [&](int th, uint64_t& ba, uint64_t& bb, int& t, uint32_t* dst) {
@@ -2708,7 +2712,8 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 int detect_rp(const Geo& g) { return g.max_rw + 3 <= 48 ? 48 : g.max_rw + 3 <= 64 ? 64 : 96; }
 
 size_t detect_lds_bytes(const Geo& g) {
-    return 2 * (size_t)detect_roi_elems(g, detect_rp(g)) + (size_t)g.fd_mp * (g.max_wh + 2) + 2 * (size_t)g.fd_pq;
+    // ROI, the M map (pitch RP bytes), the pair queue
+    return 2 * (size_t)detect_roi_elems(g, detect_rp(g)) + (size_t)detect_rp(g) * (g.max_wh + 2) + 2 * (size_t)g.fd_pq;
 }
 
 template <int RP, int NS>
