@@ -417,12 +417,13 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
     // ROI (max_rh rows x RP u16); after the M stage the same bytes stage the minTh survivors (u32 records)
     uint16_t* roi = (uint16_t*)lds;
     // u8 M map, (max_wh + 2) rows of MP = RP bytes: px (x, y) at (y + 1) * MP + x + 2, i.e. at the pair's queue
-    // entry minus 2 MP + 2
+    // entry + MP
     constexpr int MP = RP;
     uint8_t* mm = (uint8_t*)(roi + detect_roi_elems(g, RP));
-    // pair queue: entry = ROI u16 index of the pair's first pixel, (y + 3) * RP + x + 4 (x even; fd_pq
-    // entries), so the M stage's ROI and map addresses are the entry itself; the M stage compacts it in
-    // place into the NMS queue
+    // pair queue: entry = y * RP + x + 2 (x even; fd_pq entries), the ROI u16 index of the dword that holds
+    // the top-left corner of the pair's circles (ROI row y = window row y - 3, pair at ROI index
+    // entry + 3 RP + 2), so the M stage's ROI reads are the entry plus non-negative immediate offsets and its map
+    // address the entry plus MP; the M stage compacts the queue in place into the NMS queue
     uint16_t* pq = (uint16_t*)(mm + MP * (g.max_wh + 2));
     int bx, img;
     xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
@@ -594,8 +595,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     bound_at(R0 + y0 * S, colok & __builtin_amdgcn_sicmp(r, wh - y0, 40), last, ca0, cb0, aa0, ab0);
                     bound_at(R0 + (y0 + 8) * S, colok & __builtin_amdgcn_sicmp(r, wh - y0 - 8, 40), last, ca1, cb1, aa1,
                              ab1);
-                    emit((y0 + r + 3) * RP + 4 * qx + 4, ca0, cb0, aa0, ab0);
-                    emit((y0 + r + 11) * RP + 4 * qx + 4, ca1, cb1, aa1, ab1);
+                    emit((y0 + r) * RP + 4 * qx + 2, ca0, cb0, aa0, ab0);
+                    emit((y0 + r + 8) * RP + 4 * qx + 2, ca1, cb1, aa1, ab1);
                 }
             } else {
                 for (int i0 = 0; i0 < nquad; i0 += 128) {
@@ -604,8 +605,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     uint64_t ca0, cb0, ca1, cb1, aa0, ab0, aa1, ab1;
                     bound(i0 + lane, qy, 4 * qx, ca0, cb0, aa0, ab0);
                     bound(i0 + 64 + lane, qy2, 4 * qx2, ca1, cb1, aa1, ab1);
-                    emit((qy + 3) * RP + 4 * qx + 4, ca0, cb0, aa0, ab0);
-                    emit((qy2 + 3) * RP + 4 * qx2 + 4, ca1, cb1, aa1, ab1);
+                    emit(qy * RP + 4 * qx + 2, ca0, cb0, aa0, ab0);
+                    emit(qy2 * RP + 4 * qx2 + 2, ca1, cb1, aa1, ab1);
                     qy = qy2;
                     qx = qx2;
                     advance(qy, qx);
@@ -622,18 +623,18 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         auto m_stage = [&](uint16_t* qb, int dir, int n, int tl) {
             int nn = 0;
             // the queue entry of the next step is read one step ahead (its LDS round trip overlaps this step)
-            uint32_t e_next = lane < n ? qb[dir * lane] : (uint32_t)(3 * RP + 4);  // idle lanes: pixel (0, 0)
+            uint32_t e_next = lane < n ? qb[dir * lane] : 2u;  // idle lanes: pixel (0, 0)
             for (int k0 = 0; k0 < n; k0 += 64) {
                 // every lane computes (a lane past n repeats an earlier entry of its own, harmlessly); the map
                 // store and the compaction take the lanes of this step's entries (lane masks, as the pre-test)
                 const uint32_t e = e_next;
                 if (k0 + 64 + lane < n) e_next = qb[dir * (k0 + 64 + lane)];
                 const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, n, 40);  // ICMP_SLT
-                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + e));
+                const uint32_t m = fast_m_pair<S>((const uint32_t*)(roi + e) + 3 * S + 1);
                 // the u8 map keeps M itself (low byte of each biased half); odd width: the last pair's second
                 // pixel lies outside the window, its map entry is cleared after this stage
                 if (__builtin_amdgcn_inverse_ballot_w64(inr))
-                    *(uint16_t*)(mm + e - (2 * MP + 2)) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
+                    *(uint16_t*)(mm + e + MP) = (uint16_t)__builtin_amdgcn_perm(0u, m, 0x0c0c0200u);
                 // slots below k0 + 64 are written; every read of the queue (this step's entries, the next
                 // step's prefetch) was issued before
                 const uint64_t bh = inr & ((uint64_t)__builtin_amdgcn_sicmp((int)(m & 0x3FFu), tl, 38) |
@@ -659,15 +660,15 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 // every lane computes on an entry in range; lane masks select the kept pixels
                 const uint64_t inr = __builtin_amdgcn_sicmp(k0 + lane, nn, 40);  // ICMP_SLT
                 const int e = qb[dir * min(k0 + lane, nn - 1)];
-                const uint8_t* q = mm + e - (2 * MP + 2);  // pixel A = (x, y); B = (x + 1, y)
+                const uint8_t* q = mm + e + MP;  // pixel A = (x, y); B = (x + 1, y)
                 const int t_0 = q[-MP - 1], t_1 = q[-MP], t_2 = q[-MP + 1], t_3 = q[-MP + 2];
                 const int m_0 = q[-1], owna = q[0], ownb = q[1], m_3 = q[2];
                 const int b_0 = q[MP - 1], b_1 = q[MP], b_2 = q[MP + 1], b_3 = q[MP + 2];
                 const int c1 = max(t_1, b_1), c2 = max(t_2, b_2);  // the pair's columns without its own row
                 const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
                 const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
-                // (x + 3, y + 3) = (e % RP - 1, e / RP)
-                const uint32_t xy = (uint32_t)(cg.x0 + (int)((uint32_t)e % RP) - 1) | ((uint32_t)(cg.y0 + (int)((uint32_t)e / RP)) << 12);
+                // (x + 3, y + 3) = (e % RP + 1, e / RP + 3)
+                const uint32_t xy = (uint32_t)(cg.x0 + (int)((uint32_t)e % RP) + 1) | ((uint32_t)(cg.y0 + (int)((uint32_t)e / RP) + 3) << 12);
                 const uint32_t reca = xy | ((uint32_t)(owna - 1) << 24);
                 const uint32_t recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
                 auto keep = [&](int th, uint64_t& ba, uint64_t& bb, int& t, uint32_t* dst) {
