@@ -2102,6 +2102,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     }
     auto w4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | (b << 8) | (c << 16) | (d << 24); };
     auto w2 = [](uint32_t a, uint32_t b) { return __builtin_bit_cast(us2, a | (b << 16)); };
+    // results stay in registers until the wave's last keypoint: lane 4 j + i holds bits 64 i .. 64 i + 63 of
+    // keypoint j's descriptor, lane j its keypoint record.  A store inside the loop would sit in front of
+    // the next window's loads in the in-order vmcnt, and the wait for those loads then waits for the store.
+    uint32_t mine_lo = 0, mine_hi = 0, kp_x = 0, kp_y = 0, kp_angle = 0, kp_resp = 0;
     for (int j = 0; j < nk; ++j) {
         const uint32_t key = key_of(j);
         const int score = (int)(key >> 24);
@@ -2119,8 +2123,13 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             if (inside(cx)) issue(cx, cy);
         }
         // ---- horizontal taps of the disc's (row pair, group) items
+#if defined(ORBFE_X_NOH)  // experiment (tools/dbg/build_variant.sh): no horizontal pass, wrong bits
+        constexpr int kHRun = 0;
+#else
+        constexpr int kHRun = kOrbHItems;
+#endif
 #pragma unroll 1
-        for (int k = 0; k < kOrbHItems; ++k) {
+        for (int k = 0; k < kHRun; ++k) {
             if (hit[k] != ~0u) {
                 const uint32_t* q = src + (hit[k] & 0xFFFFu);
                 uint32_t h[2][4];
@@ -2148,6 +2157,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                                                           pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
             }
         }
+#if defined(ORBFE_X_NOCENT)  // experiment: no centroid / angle, wrong angles and bits
+        const float angle = 0.f, a = 1.f, b = 0.f;
+#else
         // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15)
         uint32_t a10 = 0, a01 = 0, a1 = 0;
 #pragma unroll
@@ -2163,6 +2175,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         const float angle = fast_atan2((float)m01, (float)m10);
         float b, a;
         glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
+#endif
         wave_sync_lds();  // hb complete
         // ---- steered BRIEF with the vertical taps per sample: sample (row, col) is blurred row o = row + 18
         //      (H rows o .. o + 6), column c = col + 21.  rint by the 1.5 * 2^23 trick: the f32 bits are
@@ -2176,9 +2189,13 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         typedef __attribute__((address_space(3))) const uint32_t lds_u32;
         const uint32_t kc = (uint32_t)(uintptr_t)(lds_u32*)hb + (uint32_t)(4 * (9 * kHDw + 21)) -
                             (uint32_t)(4 * kHDw) * 0xA00000u - (__float_as_uint(12582912.0f) << 2);
-        uint32_t mine_lo = 0, mine_hi = 0;  // lane i < 4 keeps bits 64 i .. 64 i + 63
+#if defined(ORBFE_X_NOBRIEF)  // experiment: no BRIEF samples, wrong bits
+        constexpr int kBRun = 0;
+#else
+        constexpr int kBRun = 4;
+#endif
 #pragma unroll 1
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kBRun; ++i) {
             const float4 pt = s_pat[lane + 64 * i];
             uint32_t v2[2];
 #pragma unroll
@@ -2205,23 +2222,29 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 v2[e] = s >> 16;
             }
             const uint64_t bb = __ballot(v2[0] < v2[1]);
-            // lane i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
+            // lane 4 j + i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
             // 3-5 % slower in round 2)
-            mine_lo = writelane_m0(mine_lo, (uint32_t)bb, i);
-            mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), i);
+            mine_lo = writelane_m0(mine_lo, (uint32_t)bb, 4 * j + i);
+            mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), 4 * j + i);
         }
-        const int o = pre[l] + k0 + j;
-        if (lane < 4) *(uint2*)(out_desc + ((int64_t)img * g.kp_cap + o) * 32 + 8 * lane) = uint2{mine_lo, mine_hi};
-        if (lane == 0) {
-            orbfe_keypoint kp;
-            kp.x = l ? __fmul_rn((float)ccx, L.scale) : (float)ccx;
-            kp.y = l ? __fmul_rn((float)ccy, L.scale) : (float)ccy;
-            kp.size = L.size;
-            kp.angle = angle;
-            kp.response = (float)score;
-            kp.octave = l;
-            out_kp[(int64_t)img * g.kp_cap + o] = kp;
+        if (lane == j) {
+            kp_x = __float_as_uint(l ? __fmul_rn((float)ccx, L.scale) : (float)ccx);
+            kp_y = __float_as_uint(l ? __fmul_rn((float)ccy, L.scale) : (float)ccy);
+            kp_angle = __float_as_uint(angle);
+            kp_resp = __float_as_uint((float)score);
         }
+    }
+    const int64_t o0 = (int64_t)img * g.kp_cap + pre[l] + k0;  // the wave's first output slot
+    if (lane < 4 * nk) *(uint2*)(out_desc + o0 * 32 + 8 * lane) = uint2{mine_lo, mine_hi};
+    if (lane < nk) {
+        orbfe_keypoint kp;
+        kp.x = __uint_as_float(kp_x);
+        kp.y = __uint_as_float(kp_y);
+        kp.size = L.size;
+        kp.angle = __uint_as_float(kp_angle);
+        kp.response = __uint_as_float(kp_resp);
+        kp.octave = l;
+        out_kp[o0 + lane] = kp;
     }
 }
 
