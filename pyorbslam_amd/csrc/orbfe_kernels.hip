@@ -2026,7 +2026,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     int stride;
     const uint8_t* lvl = level_ptr(g, l, in, in_pitch, ws, img, &stride);
     uint32_t bias;
-    const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * L.h), &bias);
+    // the level's size in SGPRs for the whole wave (a per-keypoint s_load of the kernel argument would come
+    // with an s_waitcnt lgkmcnt(0) that also drains the wave's LDS traffic)
+    const int Lw = __builtin_amdgcn_readfirstlane(L.w), Lh = __builtin_amdgcn_readfirstlane(L.h);
+    const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * Lh), &bias);
     uint32_t* src = s_src[wid];
     uint32_t* hb = s_h[wid];
     if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
@@ -2041,16 +2044,25 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     auto key_of = [&](int j) { return (uint32_t)__builtin_amdgcn_readlane((int)mykey, j); };
     // columns cx - 25 .. cx + 22 inside the level: dword staging (rows past the top / bottom are reflected
     // per item); otherwise byte loads with reflect-101 in both directions
-    auto inside = [&](int cx) { return cx >= 25 && cx + 22 < L.w; };
+    auto inside = [&](int cx) { return cx >= 25 && cx + 22 < Lw; };
     // the lane's staging item k: row it / 3, third it % 3 of the window (it = lane + 64 k)
-    auto row_off = [&](int k, int cy, bool rows_in) {  // byte offset from column cx - 25 of level row 0
+    // (row, third) offsets of the lane's items inside the window: constant per wave
+    int it_r[3];
+    uint32_t it_off[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
         const int it = min(lane + 64 * k, kStageItems - 1), r = (it * 171) >> 9, t = it - 3 * r;  // it / 3 for it < 129
-        const int y = rows_in ? cy - 21 + r : reflect101c(cy - 21 + r, L.h);
-        return (uint32_t)(y * stride + 16 * t);
+        it_r[k] = r;
+        it_off[k] = (uint32_t)(r * stride + 16 * t);
+    }
+    auto row_off = [&](int k, int cy, bool rows_in) {  // byte offset from column cx - 25 of level row cy - 21
+        if (rows_in) return it_off[k];
+        const int y = reflect101c(cy - 21 + it_r[k], Lh);
+        return (uint32_t)((y - (cy - 21)) * stride) + (it_off[k] - (uint32_t)(it_r[k] * stride));
     };
     auto issue = [&](int cx, int cy) {
-        const bool rows_in = cy >= 21 && cy + 21 < L.h;
-        const uint32_t base = (uint32_t)(cx - 25) + bias;
+        const bool rows_in = cy >= 21 && cy + 21 < Lh;
+        const uint32_t base = (uint32_t)((cy - 21) * stride + cx - 25) + bias;
         rsh = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -2083,7 +2095,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             for (int k = 0; k < NR; ++k) {
                 const int i = min(lane + 64 * (j0 + k), kSrcRows * 4 * kSrcDw - 1);
                 const int r = i / (4 * kSrcDw), c = i - r * (4 * kSrcDw);
-                const int y = reflect101c(cy - 21 + r, L.h), x = reflect101c(cx - 25 + c, L.w);
+                const int y = reflect101c(cy - 21 + r, Lh), x = reflect101c(cx - 25 + c, Lw);
                 v[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(y * stride + x) + bias, 0, 0);
             }
 #pragma unroll
