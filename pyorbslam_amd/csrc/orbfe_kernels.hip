@@ -2124,15 +2124,19 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         // ---- stage keypoint j: the previous keypoint's reads of src / hb are complete (waited before its
         //      ballots, which precede this point)
         wave_sync_lds();
+#if !defined(ORBFE_X_NOSTAGE)  // experiment: no window staging (garbage window), wrong bits
         if (inside(cx)) commit();
         else stage_border(cx, cy);
+#endif
         wave_sync_lds();
         const int ccx = cx, ccy = cy;
         if (j + 1 < nk) {  // next keypoint's loads in flight during this one's compute
             const uint32_t k = key_of(j + 1);
             cx = (int)(k & 0xFFF);
             cy = (int)((k >> 12) & 0xFFF);
+#if !defined(ORBFE_X_NOSTAGE)
             if (inside(cx)) issue(cx, cy);
+#endif
         }
         // ---- horizontal taps of the disc's (row pair, group) items
 #if defined(ORBFE_X_NOH)  // experiment (tools/dbg/build_variant.sh): no horizontal pass, wrong bits
