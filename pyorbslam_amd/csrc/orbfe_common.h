@@ -60,7 +60,10 @@ struct CellGeo {
 };
 
 // Resize column entry.
-constexpr int kRsRows = 16;  // k_resize output rows per workgroup (band)
+#ifndef ORBFE_RS_ROWS
+#define ORBFE_RS_ROWS 16  // experiment switch (tools/dbg/build_variant.sh)
+#endif
+constexpr int kRsRows = ORBFE_RS_ROWS;  // k_resize output rows per workgroup (band)
 // k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
 constexpr int kOctKeys = 7424;
 

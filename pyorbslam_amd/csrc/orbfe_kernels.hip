@@ -201,8 +201,9 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     uint4* s_sel = (uint4*)rs_lds;                       // L.rs_ngrp groups each
     uint4* s_aa = s_sel + L.rs_ngrp;
     int* s_sx0 = (int*)(s_aa + L.rs_ngrp);
-    uint32_t* s_ry = (uint32_t*)(s_sx0 + L.rs_ngrp);     // kRsRows ResizeY as 3 dwords
-    uint32_t* s_src = s_ry + 4 * kRsRows;                // staged source rows
+    // per output row of the band: LDS byte offsets of its two source rows' starts and b0 << 12, b1 << 12
+    uint4* s_ry = (uint4*)(s_sx0 + L.rs_ngrp);
+    uint32_t* s_src = (uint32_t*)(s_ry + kRsRows);       // staged source rows
     const LevelGeo& P = g.lv[l - 1];
     int bx, img;
     xcd_block(bx, img);  // neighbouring bands share source rows: keep them in one L2
@@ -234,7 +235,11 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
                 s_aa[gi] = uint4{q0.y, q0.w, q1.y, q1.w};
                 s_sx0[gi] = (int)sx0;
             }
-            if (t < 3 * nrow) s_ry[t] = ((const uint32_t*)(yt + L.ytab_off + dy0))[t];
+            if (t < nrow) {
+                const ResizeY y = yt[L.ytab_off + dy0 + t];
+                s_ry[t] = uint4{(uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride), (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride),
+                                (uint32_t)y.b0 << 12, (uint32_t)y.b1 << 12};
+            }
         }
 #pragma unroll
         for (int k = 0; k < kRsSlots; ++k) {
@@ -242,7 +247,11 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
             if (i < ndw) s_src[i] = v[k];
         }
     }
-    if (V == 2 && t < 3 * nrow) s_ry[t] = ((const uint32_t*)(yt + L.ytab_off + dy0))[t];
+    if (V == 2 && t < nrow) {
+        const ResizeY y = yt[L.ytab_off + dy0 + t];
+        s_ry[t] = uint4{(uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride), (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride),
+                        (uint32_t)y.b0 << 12, (uint32_t)y.b1 << 12};
+    }
     __syncthreads();
     uint8_t* dst = ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy0 * L.pitch;
     if (V == 1) {
@@ -253,11 +262,11 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     const int step_r = 256 / ngrp, step_g = 256 - step_r * ngrp;
     int rr = t / ngrp, grp = t - rr * ngrp;
     while (rr < nrow) {
-        const ResizeY ry = ((const ResizeY*)s_ry)[rr];
+        const uint4 ry = s_ry[rr];  // (row offset 0, row offset 1, b0 << 12, b1 << 12)
         const uint4 e = s_sel[grp], aa = s_aa[grp];
         const int sx0 = s_sx0[grp];
-        auto taps = [&](int sy, uint32_t (&h)[4]) {
-            const int A = sh0 + (sy - ys_lo) * sstride + sx0, o = A & 3;
+        auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
+            const int A = (int)roff + sx0, o = A & 3;
             const uint32_t* w = (const uint32_t*)(lsrc + (A - o));
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
             const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
@@ -272,19 +281,20 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
                                           __builtin_bit_cast(us2, aa.w), 0u, false);
         };
         uint32_t h0[4], h1[4];
-        taps(ry.sy0, h0);
-        taps(ry.sy1, h1);
+        taps(ry.x, h0);
+        taps(ry.y, h1);
         // OpenCV VResizeLinearVec_32s8u: v_mul_hi(S >> 4, beta) on int16 lanes, (x + 2) >> 2; h >> 4 <= 32640 so
-        // the int16 pack never saturates and (x * b) >> 16 == mul_hi(x, b << 16); the result is <= 255
-        const uint32_t B0 = (uint32_t)ry.b0 << 16, B1 = (uint32_t)ry.b1 << 16;
+        // the int16 pack never saturates and (x * b) >> 16 == mul_hi(x, b << 16) == mul_hi(x << 4, b << 12) ==
+        // mul_hi(h & ~15, b << 12): a (fast) v_and instead of a (4-cycle) shift; the result is <= 255
+        const uint32_t B0 = ry.z, B1 = ry.w;
         const int dx = 4 * grp;
         uint32_t v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] >> 4, B0) + __umulhi(h1[k] >> 4, B1) + 2) >> 2;
+        for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
         if (dx + 3 >= L.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (dx + k >= L.xvec) v[k] = (h0[k] * (uint32_t)ry.b0 + h1[k] * (uint32_t)ry.b1 + (1u << 21)) >> 22;
+                if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
         }
         // pixels past L.w land in the row's pitch padding
         *(uint32_t*)(dst + rr * L.pitch + dx) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
