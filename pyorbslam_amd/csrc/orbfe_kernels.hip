@@ -198,9 +198,8 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     set_prio(g, kPrioResize);
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     const LevelGeo& L = g.lv[l];
-    uint4* s_sel = (uint4*)rs_lds;                       // L.rs_ngrp groups each
-    uint4* s_aa = s_sel + L.rs_ngrp;
-    int* s_sx0 = (int*)(s_aa + L.rs_ngrp);
+    uint4* s_xa = (uint4*)rs_lds;                        // per group: v_perm selectors, then (a0, a1) weights
+    int* s_sx0 = (int*)(s_xa + 2 * L.rs_ngrp);
     // per output row of the band: LDS byte offsets of its two source rows' starts and b0 << 12, b1 << 12
     uint4* s_ry = (uint4*)(s_sx0 + L.rs_ngrp);
     uint32_t* s_src = (uint32_t*)(s_ry + kRsRows);       // staged source rows
@@ -217,6 +216,8 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     const int sh0 = (int)(a0 & 3);
     const uint32_t* gsrc = (const uint32_t*)(a0 - sh0);
     const int ndw = ((ys_hi - ys_lo) * sstride + P.w + sh0 + 3) >> 2;
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    const uint32_t src_lds = (uint32_t)(uintptr_t)(lds_u32*)s_src;  // LDS address of the staged rows
     for (int base = 0; base < (V == 2 ? 0 : ndw); base += 256 * kRsSlots) {
         uint32_t v[kRsSlots];
 #pragma unroll
@@ -231,14 +232,15 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
                 const uint32_t sx0 = q0.x;
                 // byte r and r + 1 of the window as a u16 pair (selector 0x0c = zero byte)
                 auto sel = [&](uint32_t sx) { const uint32_t r = sx - sx0; return r | ((r + 1) << 16) | 0x0c000c00u; };
-                s_sel[gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
-                s_aa[gi] = uint4{q0.y, q0.w, q1.y, q1.w};
+                s_xa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+                s_xa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
                 s_sx0[gi] = (int)sx0;
             }
             if (t < nrow) {
                 const ResizeY y = yt[L.ytab_off + dy0 + t];
-                s_ry[t] = uint4{(uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride), (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride),
-                                (uint32_t)y.b0 << 12, (uint32_t)y.b1 << 12};
+                s_ry[t] = uint4{src_lds + (uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride),
+                                src_lds + (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride), (uint32_t)y.b0 << 12,
+                                (uint32_t)y.b1 << 12};
             }
         }
 #pragma unroll
@@ -249,8 +251,8 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     }
     if (V == 2 && t < nrow) {
         const ResizeY y = yt[L.ytab_off + dy0 + t];
-        s_ry[t] = uint4{(uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride), (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride),
-                        (uint32_t)y.b0 << 12, (uint32_t)y.b1 << 12};
+        s_ry[t] = uint4{src_lds + (uint32_t)(sh0 + (y.sy0 - ys_lo) * sstride),
+                        src_lds + (uint32_t)(sh0 + (y.sy1 - ys_lo) * sstride), (uint32_t)y.b0 << 12, (uint32_t)y.b1 << 12};
     }
     __syncthreads();
     uint8_t* dst = ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy0 * L.pitch;
@@ -258,16 +260,15 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
         if (t == 0) dst[0] = ((const uint8_t*)s_src)[sh0];
         return;
     }
-    const uint8_t* lsrc = (const uint8_t*)s_src;
     const int step_r = 256 / ngrp, step_g = 256 - step_r * ngrp;
     int rr = t / ngrp, grp = t - rr * ngrp;
     while (rr < nrow) {
-        const uint4 ry = s_ry[rr];  // (row offset 0, row offset 1, b0 << 12, b1 << 12)
-        const uint4 e = s_sel[grp], aa = s_aa[grp];
+        const uint4 ry = s_ry[rr];  // (LDS address of source row 0, of row 1, b0 << 12, b1 << 12)
+        const uint4 e = s_xa[2 * grp], aa = s_xa[2 * grp + 1];
         const int sx0 = s_sx0[grp];
         auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
             const int A = (int)roff + sx0, o = A & 3;
-            const uint32_t* w = (const uint32_t*)(lsrc + (A - o));
+            lds_u32* w = (lds_u32*)(uintptr_t)(uint32_t)(A - o);
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
             const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
             // S[sx] * a0 + S[sx + 1] * a1 (a1 = 0 past xmax: OpenCV's S[sx] * 2048)
