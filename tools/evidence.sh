@@ -37,6 +37,7 @@ step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o run -- python bench.py --roofline-only --roofline-steps 2
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o run -- python bench.py --roofline-only --roofline-steps 2
 step pmc_valu 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc_valu" -o run -- python bench.py --roofline-only --roofline-steps 2
+step pmc_lds 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS --output-format csv -d "$out/pmc_lds" -o run -- python bench.py --roofline-only --roofline-steps 2
 EU="--width 752 --height 480 --nfeatures 1000"
 step pmc_fetch_euroc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch_euroc" -o run -- python bench.py --roofline-only --roofline-steps 2 $EU
 step pmc_write_euroc 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write_euroc" -o run -- python bench.py --roofline-only --roofline-steps 2 $EU
