@@ -1900,26 +1900,28 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
     *cs = (n & 1) ? sp : cp;
 }
 
-// cv::fastAtan2, plain IEEE float ops (no contraction)
-__device__ __forceinline__ float fast_atan2(float y, float x) {
+// cv::fastAtan2 of integer moments y, x (|y|, |x| < 2^24: the float conversions are exact), for
+// wave-uniform arguments: the branches are decided on the scalar unit from the integers, so only one
+// division and one polynomial are issued (a float comparison of converted values is a per-lane condition
+// to the compiler, which then issues both branches and selects).  The same IEEE float operations in the
+// same order as cv::fastAtan2 on the converted floats (plain IEEE float ops, no contraction):
+// (ax >= ay) == (|x| >= |y|), (x < 0) == (x_int < 0).
+__device__ __forceinline__ float fast_atan2_uniform(int yi, int xi) {
     const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
     const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
     const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
     const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
-    const float ax = fabsf(x), ay = fabsf(y);
-    float a;
-    if (ax >= ay) {
-        const float c = __fdiv_rn(ay, __fadd_rn(ax, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
-        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
-    } else {
-        const float c = __fdiv_rn(ax, __fadd_rn(ay, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
-        a = __fsub_rn(90.f,
-                      __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
-    }
-    if (x < 0) a = __fsub_rn(180.f, a);
-    if (y < 0) a = __fsub_rn(360.f, a);
-    return a;
+    const int axi = xi < 0 ? -xi : xi, ayi = yi < 0 ? -yi : yi;
+    const bool xge = axi >= ayi;
+    const float num = (float)(xge ? ayi : axi), den = (float)(xge ? axi : ayi);
+    const float c = __fdiv_rn(num, __fadd_rn(den, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
+    float a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    if (!xge) a = __fsub_rn(90.f, a);
+    if (xi < 0) a = __fsub_rn(180.f, a);
+    if (yi < 0) a = __fsub_rn(360.f, a);
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(a)));
 }
+
 
 
 __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clamped for far-out rows
@@ -2199,7 +2201,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             a1 = __builtin_amdgcn_udot4(m, 0x01010101u, a1, false);
         }
         const int m10 = wave_sum((int)a10 - 18 * (int)a1), m01 = wave_sum((int)a01 - 15 * (int)a1);
-        const float angle = fast_atan2((float)m01, (float)m10);
+        const float angle = fast_atan2_uniform(m01, m10);
         float b, a;
         glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
 #endif
