@@ -5,8 +5,8 @@
 //
 // Supported: bit depth 8, colour types 0 (grey), 2 (RGB), 4 (grey + alpha), 6 (RGBA), non-interlaced.  Grey
 // images are returned as stored (lossless: exact).  Colour images are converted like OpenCV's PNG decoder
-// asks libpng to (png_set_rgb_to_gray with 0.299 / 0.587: libpng's 15-bit fixed-point weights 9798, 19235,
-// 3735 and rounding, no gamma), alpha dropped — parity of that branch is unpinned (OpenCV / libpng headers
+// asks libpng to (png_set_rgb_to_gray with 0.299 / 0.587: libpng's truncated 15-bit fixed-point weights
+// 9797, 19234, 3737 and a truncating >> 15, no gamma), alpha dropped — parity of that branch is unpinned (OpenCV / libpng headers
 // are absent here).  Anything else is ORBFE_EFORMAT.
 #include <zlib.h>
 

@@ -244,6 +244,7 @@ def assign_features_to_grid(self) -> None:
     fl, o = flat.tolist(), off.tolist()
     self.mGrid = [[fl[o[ix * rows + iy]:o[ix * rows + iy + 1]] for iy in range(rows)] for ix in range(cols)]
     self._orbfe_grid = (id(self.mGrid), off, flat)
+    self._orbfe_pts = (kps, pts)  # the keypoint coordinates as doubles, for the matcher's grid queries
 
 
 def install(frame_cls, copy: bool = True, pair: bool = True) -> None:

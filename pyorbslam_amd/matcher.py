@@ -29,8 +29,10 @@ lines necessarily read like the reference's.  The two tracking searches also hav
 from __future__ import annotations
 
 import ctypes as C
+import operator
 import threading
 import weakref
+from itertools import repeat
 
 import numpy as np
 
@@ -116,6 +118,39 @@ def _is_f64(v) -> bool:
     return type(v) in _F64 or (type(v) is np.ndarray and v.dtype == np.float64 and v.size == 1)
 
 
+_DTYPE, _SIZE, _SHAPE = operator.attrgetter("dtype"), operator.attrgetter("size"), operator.attrgetter("shape")
+_F64_DT = np.dtype(np.float64)
+
+
+def _f64_array(vals: list):
+    """vals as a float64 array when every element is a double in _is_f64's sense (Python float, np.float64, or
+    a size-1 float64 ndarray: the values are taken exactly), else None.  The type checks run as map() over
+    C-level callables, not per element in Python (the tracking searches pass ~1 000 projections each)."""
+    n = len(vals)
+    if n == 0:
+        return np.zeros(0, np.float64)
+    kinds = set(map(type, vals))
+    if kinds <= _F64_SET:
+        return np.array(vals, np.float64)
+    if kinds == _NDARRAY_SET and set(map(_DTYPE, vals)) == {_F64_DT} and set(map(_SIZE, vals)) == {1}:
+        if len(set(map(_SHAPE, vals))) == 1:  # one shape: a single (n, 1[, 1]) float64 array
+            return np.array(vals, np.float64).reshape(n)
+        return np.fromiter((v.item() for v in vals), np.float64, count=n)
+    if all(_is_f64(v) for v in vals):  # a mix of the kinds above
+        return np.fromiter((v.item() if type(v) is np.ndarray else v for v in vals), np.float64, count=n)
+    return None
+
+
+_F64_SET = frozenset(_F64)
+_NDARRAY_SET = frozenset((np.ndarray,))
+_INT_SET = frozenset((int, np.int64, np.int32))
+_U8_DT = np.dtype(np.uint8)
+_UR_SET = frozenset((int, float, np.float32, np.float64))
+_DOUBLE_OR_INT_SET = frozenset((float, int, np.float64))
+_ANGLE = operator.attrgetter("angle")
+_OBSERVATIONS = operator.methodcaller("observations")
+
+
 def _frame_grid(frame):
     """(cell_off, cell_idx, kp_x, kp_y, kp_oct, frame4) of a frame, cached while its grid / keypoints are
     the same objects; None if the frame's grid parameters are not plain doubles."""
@@ -140,12 +175,38 @@ def _frame_grid(frame):
         np.cumsum(sizes, out=off[1:])
         idx = np.fromiter((g for col in frame.mGrid for cell in col for g in cell), np.int32, count=int(off[-1]))
     kps = frame.mvKeysUn
-    kx = np.fromiter((k.pt[0] for k in kps), np.float64, count=len(kps))
-    ky = np.fromiter((k.pt[1] for k in kps), np.float64, count=len(kps))
-    ko = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
+    pts = getattr(frame, "_orbfe_pts", None)  # left by frame.assign_features_to_grid: (mvKeys, (N, 2) f64)
+    if pts is not None and pts[0] is kps and kps is frame.mvKeys and len(pts[1]) == len(kps):
+        kx, ky = np.ascontiguousarray(pts[1][:, 0]), np.ascontiguousarray(pts[1][:, 1])
+        ko = _octaves(frame)
+    else:
+        kx = np.fromiter((k.pt[0] for k in kps), np.float64, count=len(kps))
+        ky = np.fromiter((k.pt[1] for k in kps), np.float64, count=len(kps))
+        ko = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
     grid = (off, idx, kx, ky, ko, np.array(f4, np.float64), cols, rows)
     _grid_cache[frame] = (key, grid)
     return grid
+
+
+_octave_cache = weakref.WeakKeyDictionary()
+
+
+def _octaves(frame) -> np.ndarray:
+    """frame.mvKeys[i].octave as an int32 array, cached while mvKeys is the same list of the same length."""
+    kps = frame.mvKeys
+    key = (id(kps), len(kps))
+    try:
+        ent = _octave_cache.get(frame)
+    except TypeError:
+        ent = None
+    if ent is not None and ent[0] == key:
+        return ent[1]
+    arr = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
+    try:
+        _octave_cache[frame] = (key, arr)
+    except TypeError:
+        pass
+    return arr
 
 
 _angle_cache = weakref.WeakKeyDictionary()
@@ -163,8 +224,9 @@ def _angles(frame):
     if ent is not None and ent[0] == key:
         return ent[1]
     arr = None
-    if all(type(k.angle) in _F64 for k in kps):
-        arr = np.fromiter((k.angle for k in kps), np.float64, count=len(kps))
+    angles = list(map(_ANGLE, kps))
+    if set(map(type, angles)) <= _F64_SET:
+        arr = np.array(angles, np.float64)
     try:
         _angle_cache[frame] = (key, arr)
     except TypeError:
@@ -227,8 +289,12 @@ def _u_right(frame, with_kinds: bool = False):
     except TypeError:
         ent = None
     if ent is None or ent[0] != (id(vals), len(vals)):
-        arr = np.fromiter((float(v) for v in vals), np.float64, count=len(vals))
-        all_double = all(type(v) in (float, int, np.float64) for v in vals)
+        kinds = set(map(type, vals))
+        if kinds <= _UR_SET:  # the values the drop-in's lists hold: -1, np.float32, Python float
+            arr = np.array(vals, np.float64)  # each value widened exactly, as float(v)
+        else:
+            arr = np.fromiter((float(v) for v in vals), np.float64, count=len(vals))
+        all_double = kinds <= _DOUBLE_OR_INT_SET
         ent = ((id(vals), len(vals)), arr, all_double)
         try:
             _uright_cache[frame] = ent
@@ -238,15 +304,34 @@ def _u_right(frame, with_kinds: bool = False):
 
 
 def _blocked(frame):
+    """Per slot of the frame: 1 if it holds a map point with observations (ORBMatcher.py's
+    `if mvpMapPoints[i]: if mvpMapPoints[i].observations() > 0: continue`)."""
     mps = frame.mvpMapPoints
-    if mps.count(None) == len(mps):
-        return np.zeros(len(mps), np.uint8)
-    return np.fromiter((1 if (m is not None and m and m.observations() > 0) else 0 for m in mps), np.uint8,
-                       count=len(mps))
+    n = len(mps)
+    out = np.zeros(n, np.uint8)
+    if mps.count(None) == n:
+        return out
+    held = np.flatnonzero(np.fromiter(map(operator.is_not, mps, repeat(None, n)), bool, count=n))
+    hl = held.tolist()
+    out[held] = _obs_flags([mps[i] for i in hl])
+    return out
 
 
 def _obs_flags(mps) -> np.ndarray:
+    """1 per map point that is truthy and has observations() > 0."""
+    if all(mps):
+        obs = list(map(_OBSERVATIONS, mps))
+        if set(map(type, obs)) <= _INT_SET:
+            return (np.array(obs, np.int64) > 0).astype(np.uint8)
     return np.fromiter((1 if (m and m.observations() > 0) else 0 for m in mps), np.uint8, count=len(mps))
+
+
+def _descriptor_rows(descs: list) -> np.ndarray:
+    """(n, 32) u8 array of n map-point descriptors (one array copy when they are all 32-byte u8 arrays)."""
+    if (set(map(type, descs)) == _NDARRAY_SET and set(map(_DTYPE, descs)) == {_U8_DT}
+            and set(map(_SIZE, descs)) == {32} and len(set(map(_SHAPE, descs))) == 1):
+        return np.array(descs, np.uint8).reshape(len(descs), 32)
+    return np.stack([np.asarray(d, np.uint8).reshape(32) for d in descs])
 
 
 class ORBMatcher:
@@ -295,29 +380,32 @@ class ORBMatcher:
         np.cumsum(cnt[rows], out=off2[1:])
         if len(rows) == 0:
             return rows, off2, np.zeros(0, np.int32)
-        qd = np.stack([np.asarray(pmps[r].get_descriptor(), np.uint8).reshape(32) for r in rows.tolist()])
+        qd = _descriptor_rows([pmps[r].get_descriptor() for r in rows.tolist()])
         return rows, off2, np.ascontiguousarray(self._csr(qd, train, off2, idx), np.int32)
 
     # ORBMatcher.py:215-283
     def search_by_projection_f_p(self, frame, vp_map_points, th):
         n_matches = 0
         b_factor = th != 1.0
-        pend, queries = [], []
+        radius = self.radius_by_viewing_cos
+        pmps, lvls, rads = [], [], []
         for pMP in vp_map_points:
             if not pMP.mbTrackInView:
                 continue
             if pMP.is_bad():
                 continue
-            n_predicted_level = pMP.mnTrackScaleLevel
-            r = self.radius_by_viewing_cos(pMP.mTrackViewCos)
+            r = radius(pMP.mTrackViewCos)
             if b_factor:
                 r *= th
-            pend.append((pMP, n_predicted_level, r))
-            queries.append((pMP.mTrackProjX, pMP.mTrackProjY, r * frame.mvScaleFactors[n_predicted_level],
-                            n_predicted_level - 1, n_predicted_level))
-        done = self._f_p_native(frame, pend, queries)
+            pmps.append(pMP)
+            lvls.append(pMP.mnTrackScaleLevel)
+            rads.append(r)
+        done = self._f_p_native(frame, pmps, lvls, rads)
         if done is not None:
             return done
+        sf = frame.mvScaleFactors
+        pend = list(zip(pmps, lvls, rads))
+        queries = [(p.mTrackProjX, p.mTrackProjY, r * sf[lv], lv - 1, lv) for p, lv, r in pend]
         work = [(pMP, lvl, r, v_indices, pMP.get_descriptor())
                 for (pMP, lvl, r), v_indices in zip(pend, features_in_areas(frame, queries)) if v_indices]
         dists = self._batched([(w[4], w[3]) for w in work], frame.mDescriptors)
@@ -366,10 +454,15 @@ class ORBMatcher:
         b_backward = -tlc[2] > current_frame.mb
         # projection of every usable map point of the last frame (one stacked matmul: the same per-point
         # BLAS product as `Rcw @ x3Dw`, element-wise arithmetic in the reference's order and dtypes)
-        cand = [i for i in range(last_frame.N) if last_frame.mvpMapPoints[i] and not last_frame.mvbOutlier[i]]
-        pos = [last_frame.mvpMapPoints[i].get_world_pos() for i in cand]
+        lmps, lout, n_last = last_frame.mvpMapPoints, last_frame.mvbOutlier, last_frame.N
+        if len(lmps) >= n_last and len(lout) >= n_last:
+            cand = [i for i, m, o in zip(range(n_last), lmps, lout) if m and not o]
+        else:  # the reference's indexing (and its IndexError)
+            cand = [i for i in range(n_last) if lmps[i] and not lout[i]]
+        pos = [lmps[i].get_world_pos() for i in cand]
         proj = []
-        if pos and all(type(p) is np.ndarray and p.shape == (3, 1) and p.dtype == pos[0].dtype for p in pos):
+        if (pos and set(map(type, pos)) == _NDARRAY_SET and set(map(_SHAPE, pos)) == {(3, 1)}
+                and len(set(map(_DTYPE, pos))) == 1):
             x3Dc = Rcw @ np.stack(pos) + tcw
             zc = x3Dc[:, 2, 0]
             invzc = 1.0 / zc
@@ -457,37 +550,48 @@ class ORBMatcher:
     # None, before touching anything, when an operand has another type (float32 projections promote
     # differently under NumPy 2): the caller then runs the Python loop.
 
-    def _f_p_native(self, frame, pend, queries):
+    def _f_p_native(self, frame, pmps, lvls, rads):
+        """pmps / lvls / rads: the searched map points (tracked in view, not bad), their predicted levels and
+        radii; the window of each is (mTrackProjX, mTrackProjY, r * mvScaleFactors[level], level - 1,
+        level) as in the reference loop."""
         grid = _frame_grid(frame)
-        if grid is None or not queries:
+        if grid is None or not pmps:
             return None
-        if not all(_is_f64(x) and _is_f64(y) and _is_f64(r) for x, y, r, _, _ in queries):
+        if not (set(map(type, lvls)) <= _INT_SET and set(map(type, rads)) <= _F64_SET):
             return None
-        pmps = [p for p, _, _ in pend]
+        sf = frame.mvScaleFactors
+        if not set(map(type, sf)) <= _F64_SET:
+            return None
+        n = len(pmps)
+        lo_hi = np.array(lvls, np.int64)
+        if lo_hi.min() < -len(sf) or lo_hi.max() >= len(sf):
+            return None
+        qr = np.array(rads, np.float64) * np.array(sf, np.float64)[lo_hi]  # r * mvScaleFactors[level], doubles
+        qx = _f64_array([p.mTrackProjX for p in pmps])
+        if qx is None:
+            return None
+        qy = _f64_array([p.mTrackProjY for p in pmps])
+        if qy is None:
+            return None
         xr_all = [p.mTrackProjXR for p in pmps]
-        if not all(_is_f64(x) for x in xr_all):
+        xr_arr = _f64_array(xr_all)
+        if xr_arr is None:
             return None
         n_frame = len(frame.mvpMapPoints)
         u_right, u_double = _u_right(frame, with_kinds=True)
         # ORBMatcher.py's er = abs(XR - mvuRight[idx]): a Python-float XR against an np.float32 entry
         # evaluates in float32 (NEP 50), which the double selection in C does not reproduce
-        if not u_double and any(type(x) is float for x in xr_all):
+        if not u_double and float in set(map(type, xr_all)):
             return None
         if len(u_right) != n_frame or len(grid[4]) != n_frame:
             return None
-        n = len(queries)
-        f64 = lambda v: v.item() if type(v) is np.ndarray else v  # noqa: E731  (size-1 float64: .item() is exact)
-        qx = np.fromiter((f64(q[0]) for q in queries), np.float64, count=n)
-        qy = np.fromiter((f64(q[1]) for q in queries), np.float64, count=n)
-        qr = np.fromiter((f64(q[2]) for q in queries), np.float64, count=n)
-        lo = np.fromiter((q[3] for q in queries), np.int32, count=n)
-        hi = np.fromiter((q[4] for q in queries), np.int32, count=n)
-        off, idx = _grid_csr(frame, grid, qx, qy, qr, lo, hi)
+        lv32 = lo_hi.astype(np.int32)
+        off, idx = _grid_csr(frame, grid, qx, qy, qr, lv32 - 1, lv32)
         rows, off2, dist = self._nonempty(off, idx, pmps, frame.mDescriptors)
         if len(rows) == 0:
             return 0
         rl = rows.tolist()
-        xr = np.fromiter((f64(xr_all[r]) for r in rl), np.float64, count=len(rl))
+        xr = np.ascontiguousarray(xr_arr[rows])
         rs = np.ascontiguousarray(qr[rows])
         q_obs = _obs_flags([pmps[r] for r in rl])
         blocked = _blocked(frame)
@@ -514,7 +618,7 @@ class ORBMatcher:
         if len(u_right) != n_frame:
             return None
         ci = np.asarray(cand, np.int64)[sel].tolist()
-        octv = np.fromiter((last.mvKeys[i].octave for i in ci), np.int32, count=len(ci))
+        octv = _octaves(last)[np.asarray(ci, np.int64)] if ci else np.zeros(0, np.int32)
         radius = th * np.asarray(sf, np.float64)[octv]  # th * mvScaleFactors[octave], one double product each
         if b_forward:
             lo, hi = octv, np.full(len(ci), -1, np.int32)

@@ -48,6 +48,15 @@ def test_grid_matches_reference(seed):
         for iy, cell in enumerate(col):
             c = ix * rows + iy
             assert flat[off[c]:off[c + 1]].tolist() == cell
+    # the matcher's grid arrays from the coordinates the drop-in kept equal the ones read from the keypoints
+    from pyorbslam_amd import matcher as M
+    new.mvKeysUn = new.mvKeys
+    kept = M._frame_grid(new)
+    ref.mvKeysUn, ref.mGrid = ref.mvKeys, new.mGrid
+    read = M._frame_grid(ref)  # no _orbfe_grid / _orbfe_pts: rebuilt from mGrid and the KeyPoint objects
+    assert new._orbfe_pts[0] is new.mvKeys and not hasattr(ref, "_orbfe_pts")
+    for a, b in zip(kept[:6], read[:6]):
+        assert a.dtype == b.dtype and np.array_equal(a, b)
 
 
 def test_grid_empty_frame_runs_reference():
