@@ -15,8 +15,9 @@ Default (--mode throughput), the BASELINE.json metric:
   their status; under torchrun, WORLD_SIZE must equal --gpus (exit 2 otherwise).
 
   Beside `value` (never replacing it), each untimed or separately timed:
-  * parity of the bench's own workload: every handle's overflow word, first / last pair of every handle
-    bit for bit against the oracle extractor and the stereo restatement;
+  * parity of the bench's own workload: every handle's overflow word, 64 pairs per rank (first, last and
+    evenly spaced pairs of every handle) bit for bit against the oracle extractor and the stereo
+    restatement (the oracle on a thread pool);
   * with_gather (N > 1): k_pack of every pair's record + one RCCL gather to rank 0, timed like a step;
   * c4_strong: the C4 configuration (64 pairs in total, sharded over the N ranks) timed like a step, plus
     its gather when N > 1, so every N of the driver's scaling run records the C4 curve;
@@ -177,43 +178,50 @@ def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, pro
 
 
 # ------------------------------------------------------------------------------------------ parity check
-def parity_check(fes, counts, host, width, height, nfeatures):
-    """First and last pair of every handle against the oracle extractor and the stereo restatement, bit for
-    bit; every handle's overflow word.  Returns (pairs checked, max overflow word, failures)."""
+def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64):
+    """About `pairs_total` pairs of the timed batch (per handle: its first and last pair and evenly spaced
+    ones between) against the oracle extractor and the stereo restatement, bit for bit; every handle's
+    overflow word.  The device results are fetched first; the oracle runs on a thread pool (its C calls
+    release the GIL and keep their state per thread).  Returns (pairs checked, max overflow word, failures)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import stereo_oracle
     from oracle.oracle import OracleExtractor
     from pyorbslam_amd.batch import KITTI_BF, KITTI_FX
     from pyorbslam_amd.frame import to_reference_lists
-    checked, ovf, bad = 0, 0, []
-    oL, oR = OracleExtractor(nfeatures=nfeatures), OracleExtractor(nfeatures=nfeatures)
-    t = oL.tables()
+    ovf, jobs = 0, []
+    per = max(2, -(-pairs_total // max(len(fes), 1)))
     first = 0
     for hi, (f, n) in enumerate(zip(fes, counts)):
         ovf = max(ovf, f.overflow())
-        for p in sorted({0, n - 1}) if n else []:
+        for p in (np.unique(np.linspace(0, n - 1, min(per, n)).round().astype(int)).tolist() if n else []):
             g = first + p  # pair index inside this rank's batch
-            L, R = host[2 * g], host[2 * g + 1]
-            kl, dl = oL.extract(L)
-            kr, dr = oR.extract(R)
-            gk, gd = f.fetch_image(2 * p)
-            hk, hd = f.fetch_image(2 * p + 1)
-            if gk.tobytes() != kl.tobytes() or not np.array_equal(gd, dl) or hk.tobytes() != kr.tobytes() \
-                    or not np.array_equal(hd, dr):
-                bad.append(f"handle {hi} pair {p}: extraction differs from the oracle")
-                continue
-            res = f.fetch_stereo(p)
-            u, d = to_reference_lists(res, gk, KITTI_BF)
-            ou, od, _ = stereo_oracle.compute_stereo_matches(kl, kr, dl, dr, oL.sheared_pyramid(), oR.sheared_pyramid(),
-                                                             t["scale"], t["inv_scale"], KITTI_BF, np.float32(KITTI_FX))
-            for a, b in ((u, ou), (d, od)):
-                sa, va = stereo_oracle.encode(a)
-                sb, vb = stereo_oracle.encode(b)
-                if not (np.array_equal(sa, sb) and np.array_equal(va, vb)):
-                    bad.append(f"handle {hi} pair {p}: stereo differs from the restatement")
-                    break
-            checked += 1
+            jobs.append((hi, p, host[2 * g], host[2 * g + 1], f.fetch_image(2 * p), f.fetch_image(2 * p + 1),
+                         f.fetch_stereo(p)))
         first += n
-    return checked, ovf, bad
+
+    def check(job):
+        hi, p, L, R, (gk, gd), (hk, hd), res = job
+        oL, oR = OracleExtractor(nfeatures=nfeatures), OracleExtractor(nfeatures=nfeatures)
+        t = oL.tables()
+        kl, dl = oL.extract(L)
+        kr, dr = oR.extract(R)
+        if gk.tobytes() != kl.tobytes() or not np.array_equal(gd, dl) or hk.tobytes() != kr.tobytes() \
+                or not np.array_equal(hd, dr):
+            return f"handle {hi} pair {p}: extraction differs from the oracle"
+        u, d = to_reference_lists(res, gk, KITTI_BF)
+        ou, od, _ = stereo_oracle.compute_stereo_matches(kl, kr, dl, dr, oL.sheared_pyramid(), oR.sheared_pyramid(),
+                                                         t["scale"], t["inv_scale"], KITTI_BF, np.float32(KITTI_FX))
+        for a, b in ((u, ou), (d, od)):
+            sa, va = stereo_oracle.encode(a)
+            sb, vb = stereo_oracle.encode(b)
+            if not (np.array_equal(sa, sb) and np.array_equal(va, vb)):
+                return f"handle {hi} pair {p}: stereo differs from the restatement"
+        return None
+
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))  # the box's CPU share for one GPU
+    with ThreadPoolExecutor(workers) as ex:
+        bad = [r for r in ex.map(check, jobs) if r is not None]
+    return len(jobs), ovf, bad
 
 
 # ---------------------------------------------------------------------------------------------- frame mode
@@ -502,6 +510,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = this "
                     "job's CPU share, at most 16)")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity check of the bench workload")
+    ap.add_argument("--parity-pairs", type=int, default=64,
+                    help="pairs of the timed batch checked against the oracle after the timed region (per rank)")
     ap.add_argument("--roofline-steps", type=int, default=5, help="steps of the standalone per-stage pass (0 = skip)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the standalone per-stage pass (for rocprofv3 --pmc runs whose dispatches must all be "
@@ -571,7 +581,8 @@ def main():
     # ---- parity of the bench's own workload (untimed)
     parity = None
     if sh is not None and not args.no_parity:
-        checked, ovf, bad = parity_check(sh.fes, sh.counts, host, args.width, args.height, args.nfeatures)
+        checked, ovf, bad = parity_check(sh.fes, sh.counts, host, args.width, args.height, args.nfeatures,
+                                         args.parity_pairs)
         if world > 1:
             t = torch.tensor([len(bad), ovf, checked], dtype=torch.int64)
             t = t.to(dev) if dist.get_backend() == "nccl" else t

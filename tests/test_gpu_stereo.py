@@ -294,8 +294,8 @@ def test_undistort_keypoints_drop_in():
 
 def test_default_bench_configuration_sampled():
     """The exact default bench step (bench.Shard: 512 KITTI pairs as 4 handles x 128 pairs on 4 streams, lanes
-    1) and the bench's own parity check: every handle's overflow word, its first and last pair bit for bit
-    against the oracle extractor and the stereo restatement."""
+    1) and the bench's own parity check: every handle's overflow word, 16 pairs of every handle (first, last and
+    evenly spaced between) bit for bit against the oracle extractor and the stereo restatement."""
     torch = pytest.importorskip("torch")
     import bench
     P, S = 512, 4
@@ -307,7 +307,7 @@ def test_default_bench_configuration_sampled():
         sh.step()
     torch.cuda.synchronize()
     checked, ovf, bad = bench.parity_check(sh.fes, sh.counts, host, 1241, 376, 2000)
-    assert ovf == 0 and not bad and checked == 8, bad
+    assert ovf == 0 and not bad and checked == 64, bad
 
 
 def test_c4_shards_and_host_fed():
