@@ -1,5 +1,5 @@
-"""Debug aid: cProfile of the two tracking searches alone (search_by_projection_f_f / _f_p) inside the C3
-replay on the GPU box; prints the searches' wall times and the profile of those calls only."""
+"""Debug aid: cProfile of the C3 replay's timed calls alone (the Frame constructor, search_by_projection_f_f /
+_f_p) on the GPU box; prints their wall times and the profile of those calls only (argv[2]: sort key)."""
 import cProfile
 import json
 import pstats
@@ -19,7 +19,7 @@ g = H.load_golden()
 meta = json.loads(str(g["meta"]))
 seq = synth.StereoSequence(meta["seq"]["seed"], meta["width"], meta["height"], meta["seq"]["speed"])
 prof = cProfile.Profile()
-T = {"f_f": [], "f_p": []}
+T = {"f_f": [], "f_p": [], "frame": []}
 on = [False]
 
 
@@ -46,7 +46,15 @@ class PM(ORBMatcher):
 
 
 class DropInFrame(H.SeqFrame):
-    pass
+    def __init__(self, *a, **k):
+        if on[0]:
+            prof.enable()
+        t = time.perf_counter()
+        try:
+            super().__init__(*a, **k)
+        finally:
+            prof.disable()
+            T["frame"].append(time.perf_counter() - t)
 
 
 F.install(DropInFrame)
@@ -58,4 +66,4 @@ for k, v in T.items():
     print(k, "median ms (unprofiled)", round(1e3 * sorted(v)[len(v) // 2], 3))
 on[0] = True
 H.replay(g, seq, ex, PM, DropInFrame, n_frames=n)
-pstats.Stats(prof).sort_stats("tottime").print_stats(30)
+pstats.Stats(prof).sort_stats(sys.argv[2] if len(sys.argv) > 2 else "tottime").print_stats(40)
