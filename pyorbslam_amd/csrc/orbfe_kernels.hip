@@ -52,14 +52,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc(const void* p, ui
                                              0x00020000);
 }
 
-// The same for a pointer that may differ between lanes (the compiler waterfalls the load over the
-// distinct resources).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc_lane(const void* p, uint32_t nbytes, uint32_t* bias) {
-    const uint64_t a = (uint64_t)(uintptr_t)p;
-    *bias = (uint32_t)a & 3u;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(a & ~(uint64_t)3), 0, nbytes + *bias, 0x00020000);
-}
-
 // Wave-wide sum (wave-uniform result): DPP quad_perm / row_ror sums inside each 16-lane row, then the
 // four row sums through v_readlane (no LDS-crossbar round trips).
 __device__ __forceinline__ int wave_sum(int v) {
@@ -2411,56 +2403,20 @@ __device__ __forceinline__ uint32_t row16_min(uint32_t v) {
     return v;
 }
 
-// n consecutive pixels (row r, columns c0 ..) of the sheared view of a level -> dst
-__device__ __forceinline__ void sheared_row(const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
-                                            uint8_t* dst) {
-    const int pw = w + 2 * kEdge;
-    const int f = kEdge * pw + kEdge + r * w + c0;
-    int pr = f / pw, pc = f - pr * pw;
-    if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
-        // the run lies inside one row of the level (the common case): 6 dword loads from the aligned
-        // start, bounded to the level (reads past its end return 0), bytes re-aligned with v_alignbyte
-        uint32_t bias;  // lvl differs between the 16-lane groups of a wave (one keypoint and octave each)
-        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc_lane(lvl, (uint32_t)(stride * h), &bias);
-        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge)) + bias;
-        const uint32_t sh = off & 3u, al = off - sh;
-        uint32_t d[7];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * k, 0, 0);
-        d[6] = 0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t wd = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (4 * k + b < n) dst[4 * k + b] = (uint8_t)(wd >> (8 * b));
-        }
-        return;
-    }
-    uint8_t v[21];
-#pragma unroll
-    for (int j = 0; j < 21; ++j) {
-        if (j < n) v[j] = lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)];
-        if (++pc == pw) {
-            pc = 0;
-            ++pr;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 21; ++j)
-        if (j < n) dst[j] = v[j];
-}
-
-// sheared_row's run of n <= 24 bytes, returned as 6 dwords (byte j of the run = byte j % 4 of w[j / 4])
-__device__ __forceinline__ void sheared_words(const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
+// n <= 24 consecutive pixels (row r, columns c0 ..) of the sheared view of a level as 6 dwords (byte j of the run = byte j % 4 of w[j / 4]).
+// rs: a wave-uniform resource over the buffer holding the level (the pair's input image or its workspace),
+// bias its base misalignment, lvl_off the level's byte offset in it (per lane): the loads need no
+// per-lane resource (a per-lane one makes the compiler waterfall every load over the wave's distinct
+// resources).  Bytes of the 24 past the run are whatever follows it in the buffer (0 past its end);
+// k_stereo masks them.  lvl: the level itself, for the reflect-101 path at its border.
+__device__ __forceinline__ void sheared_words(__amdgpu_buffer_rsrc_t rs, uint32_t bias, uint32_t lvl_off,
+                                              const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
                                               uint32_t (&wd)[6]) {
     const int pw = w + 2 * kEdge;
     const int f = kEdge * pw + kEdge + r * w + c0;
     int pr = f / pw, pc = f - pr * pw;
     if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
-        uint32_t bias;  // lvl differs between the 16-lane groups of a wave (one keypoint and octave each)
-        const __amdgpu_buffer_rsrc_t rs = aligned_rsrc_lane(lvl, (uint32_t)(stride * h), &bias);
-        const uint32_t off = (uint32_t)((pr - kEdge) * stride + (pc - kEdge)) + bias;
+        const uint32_t off = bias + lvl_off + (uint32_t)((pr - kEdge) * stride + (pc - kEdge));
         const uint32_t sh = off & 3u, al = off - sh;
         uint32_t d[7];
 #pragma unroll
@@ -2518,6 +2474,16 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     const uint8_t* DL = A.descL + pr * A.kp_stride * 32;
     const uint8_t* DR = A.descR + pr * A.kp_stride * 32;
     const float2* rinfo = A.rinfo + pr * A.out_stride;
+    // the pair's two input images and two workspaces (levels >= 1) as wave-uniform buffer resources
+    const uint8_t* lvl0L = A.lvl0L + pr * A.lvl0_stride;
+    const uint8_t* lvl0R = A.lvl0R + pr * A.lvl0_stride;
+    const uint8_t* wsL = A.wsL + pr * A.ws_stride;
+    const uint8_t* wsR = A.wsR + pr * A.ws_stride;
+    uint32_t bL0, bR0, bLW, bRW;
+    const uint32_t img_bytes = (uint32_t)g.W * (uint32_t)g.H;
+    const __amdgpu_buffer_rsrc_t rsL0 = aligned_rsrc(lvl0L, img_bytes, &bL0), rsR0 = aligned_rsrc(lvl0R, img_bytes, &bR0);
+    const __amdgpu_buffer_rsrc_t rsLW = aligned_rsrc(wsL, (uint32_t)g.ws_bytes, &bLW),
+                                 rsRW = aligned_rsrc(wsR, (uint32_t)g.ws_bytes, &bRW);
     if (sl < 11) sad[kq][sl] = 0;
     uint32_t key = 0xFFFFFFFFu;  // (distance << 16) | iR
     // the left record is read before the count is known (iL < kp_cap: inside the array), so the two
@@ -2580,12 +2546,12 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         const uint8_t *lvlL, *lvlR;
         int lstride;
         if (oct == 0) {
-            lvlL = A.lvl0L + pr * A.lvl0_stride;
-            lvlR = A.lvl0R + pr * A.lvl0_stride;
+            lvlL = lvl0L;
+            lvlR = lvl0R;
             lstride = g.W;
         } else {
-            lvlL = A.wsL + pr * A.ws_stride + s_wsoff[oct];
-            lvlR = A.wsR + pr * A.ws_stride + s_wsoff[oct];
+            lvlL = wsL + s_wsoff[oct];
+            lvlR = wsR + s_wsoff[oct];
             lstride = s_pitch[oct];
         }
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
@@ -2593,8 +2559,14 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
                  scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
         if (do_sad && sl < 11) {  // lane sl stages window row sl
             uint32_t wl[6], wr[6];
-            sheared_words(lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, wl);
-            sheared_words(lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, wr);
+            if (oct == 0) {
+                sheared_words(rsL0, bL0, 0u, lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, wl);
+                sheared_words(rsR0, bR0, 0u, lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, wr);
+            } else {
+                const uint32_t lo = (uint32_t)s_wsoff[oct];
+                sheared_words(rsLW, bLW, lo, lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, wl);
+                sheared_words(rsRW, bRW, lo, lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, wr);
+            }
             constexpr uint32_t k512 = 0x02000200u;
             // bytes (b, b + 1) of a dword pair as two u16 (0x0c selects a zero byte)
             auto lo2 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c010c00u); };
