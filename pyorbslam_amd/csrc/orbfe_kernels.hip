@@ -300,6 +300,108 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
     }
 }
 
+// k_resize_rows: the same band, with the compute mapped so that a wave's row is uniform.  The block holds
+// R_s row sets of W_g waves (64 W_g >= the level's groups): lane (w % W_g) * 64 + lane of a set owns one
+// 4-pixel group for the whole band, its x selectors / weights in registers; set w / W_g takes rows
+// set, set + R_s, ...  A row's source-row LDS addresses and vertical weights come from scalar loads of the
+// y table, the store is a buffer store with the row offset in soffset: per 4 pixels only the taps, the
+// vertical rounding and the pack are VALU work (k_resize's per-item row / table LDS reads, index wrap
+// and 64-bit store address are gone).  Blocks of 256 <= 64 W_g R_s <= 512 threads (the host picks R_s).
+__global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                                     uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
+                                                     const ResizeY* __restrict__ yt, int wg) {
+    set_prio(g, kPrioResize);
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
+    uint32_t* s_src = (uint32_t*)rs_lds;  // staged source rows
+    const LevelGeo& L = g.lv[l];
+    const LevelGeo& P = g.lv[l - 1];
+    int bx, img;
+    xcd_block(bx, img);
+    const int t = threadIdx.x, nthr = blockDim.x;
+    const int dy0 = bx * kRsRows, nrow = min(kRsRows, L.h - dy0);
+    const int ngrp = (L.w + 3) >> 2;
+    int sstride;
+    const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
+    const ResizeY* yb = yt + L.ytab_off + dy0;
+    const int ys_lo = yb[0].sy0, ys_hi = yb[nrow - 1].sy1;
+    const uintptr_t a0 = (uintptr_t)(src + (int64_t)ys_lo * sstride);
+    const int sh0 = (int)(a0 & 3);
+    const uint32_t* gsrc = (const uint32_t*)(a0 - sh0);
+    const int ndw = ((ys_hi - ys_lo) * sstride + P.w + sh0 + 3) >> 2;
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    const uint32_t src_lds = (uint32_t)(uintptr_t)(lds_u32*)s_src;
+    // this thread's group: x selectors / weights straight from the table (issued with the staging loads)
+    const int wv = t >> 6, set = __builtin_amdgcn_readfirstlane(wv / wg), nset = nthr / (64 * wg);
+    const int grp = (wv - set * wg) * 64 + (t & 63);
+    const bool own = grp < ngrp;
+    uint4 e{}, aa{};
+    int sx0 = 0;
+    if (own) {
+        const uint4* xg = (const uint4*)(xt + L.xtab_off);
+        const uint4 q0 = xg[2 * grp], q1 = xg[2 * grp + 1];
+        sx0 = (int)q0.x;
+        auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
+        e = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+        aa = uint4{q0.y, q0.w, q1.y, q1.w};
+    }
+    // staging by the first 256 threads (blocks have >= 256): compile-time strides, immediate LDS offsets
+    if (t < 256) {
+        for (int base = 0; base < ndw; base += 256 * kRsSlots) {
+            uint32_t v[kRsSlots];
+#pragma unroll
+            for (int k = 0; k < kRsSlots; ++k) {
+                const int i = base + t + 256 * k;
+                v[k] = i < ndw ? gsrc[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kRsSlots; ++k) {
+                const int i = base + t + 256 * k;
+                if (i < ndw) s_src[i] = v[k];
+            }
+        }
+    }
+    __syncthreads();
+    if (!own) return;
+    uint8_t* dst = ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy0 * L.pitch;
+    const __amdgpu_buffer_rsrc_t rd = uniform_rsrc(dst);
+    const int dx = 4 * grp;
+    const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
+    const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
+    for (int rr = set; rr < nrow; rr += nset) {
+        const ResizeY y = yb[rr];  // uniform: scalar loads
+        const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
+        const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
+        auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
+            const uint32_t A = lsrc + roff, o = A & 3u;
+            lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+            h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
+                                          __builtin_bit_cast(us2, aa.x), 0u, false);
+            h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
+                                          __builtin_bit_cast(us2, aa.y), 0u, false);
+            h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
+                                          __builtin_bit_cast(us2, aa.z), 0u, false);
+            h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                          __builtin_bit_cast(us2, aa.w), 0u, false);
+        };
+        uint32_t h0[4], h1[4];
+        taps(r0, h0);
+        taps(r1, h1);
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
+        if (tail) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+        }
+        // pixels past L.w land in the row's pitch padding
+        __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
+                                              (uint32_t)(rr * L.pitch), 0);
+    }
+}
+
 // ------------------------------------------------------------------------------- k_detect
 // One wavefront per (cell, image).  FAST "M" of a pixel:
 //   M = max(v - min_arc max9, max_arc min9 - v) over the 16 arcs of 9 contiguous circle pixels;
@@ -2728,8 +2830,18 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
                          const ResizeY* yt, int n_images, hipStream_t s, int variant) {
     dim3 grid((g.lv[l].h + kRsRows - 1) / kRsRows, n_images);
     const LevelGeo& L = g.lv[l];  // LDS sized for this level (tables + its bands' source rows)
+    // production: k_resize_rows (profiles/r03/resize_rows_ab_r3f.log: 414 -> 394 us per 256 pairs
+    // standalone, +0.8 % on the 4-handle step); variants (tools/microbench.py): 4 = the item-mapped
+    // k_resize, 1 / 2 = its staging-only / compute-only ablations
+    if (variant == 0 || variant == 3) {
+        const int ngrp = (L.w + 3) / 4, wg = (ngrp + 63) / 64;
+        const int sets = (4 + wg - 1) / wg;  // row sets: >= 256 threads per block (the staging threads)
+        hipLaunchKernelGGL(k_resize_rows, grid, dim3(64 * wg * sets), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in,
+                           in_pitch, ws, xt, yt, wg);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
-    auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;
+    auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;  // variant 4: k_resize<0>
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();
 }

@@ -11,7 +11,7 @@ import json
 import sys
 from pathlib import Path
 
-STAGES = {"resize": ["k_resize"], "detect": ["k_detect"], "octree": ["k_octree_bins", "k_octree"],
+STAGES = {"resize": ["k_resize_rows", "k_resize"], "detect": ["k_detect"], "octree": ["k_octree_bins", "k_octree"],
           "describe": ["k_orb"], "stereo": ["k_stereo_bucket", "k_stereo"]}
 
 
