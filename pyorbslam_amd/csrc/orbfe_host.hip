@@ -504,7 +504,12 @@ std::vector<uint32_t> orb_tables(const int* umax) {
             if (n >= 192) throw Error(ORBFE_EINVAL, "k_orb: more than 192 horizontal items");
             t[n++] = (uint32_t)(2 * m * 12 + gx) | ((uint32_t)(m * 10 + gx) << 16);
         }
-    for (; n < 192; ++n) t[n] = ~0u;
+    // lanes without an item run a dummy one: source dword 0, H slot (row pair 0, group 0) — a corner of the
+    // window no BRIEF sample reaches, so k_orb needs no per-item test
+    for (int rr = 0; rr < 2; ++rr)
+        for (int c = 0; c < 4; ++c)
+            if (need[rr][c]) throw Error(ORBFE_EINVAL, "k_orb: the dummy H slot lies on the sample disc");
+    for (; n < 192; ++n) t[n] = 0u;
     uint32_t* cw = t.data() + 192;
     int sl = 0;
     for (int r = 0; r < 31; ++r) {

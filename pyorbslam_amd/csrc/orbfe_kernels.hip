@@ -574,8 +574,9 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             const int n8 = (rw + 8) >> 3;  // 8-column groups of columns -1 .. rw-1 (8 * n8 <= RP)
 #pragma unroll
             for (int k = 0; k < NS2; ++k) {
-                // every lane takes part in the DPP (uniform control flow); lanes 15 of a DPP row get 0
-                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)raw[k].x, 0x101, 0xF, 0xF, false);
+                // every lane takes part in the DPP (uniform control flow); lanes 15 of a DPP row get 0 (bound_ctrl:
+                // the same 0 as an `old` operand, without the v_mov that would materialise it)
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)raw[k].x, 0x101, 0xF, 0xF, true);
                 const int r = r0 + 8 * k;
                 if (r < rh && d < n8) {
                     const int sh = (int)((lvl_lo + off0 + (uint32_t)(8 * k * stride)) & 3u);
@@ -2101,7 +2102,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         const uint4 c = i < 64 * kOrbCSlots ? ((const uint4*)(tab + 192))[i] : uint4{};
         cw_r[k] = uint2{c.x, c.y};
     }
-    uint32_t hit[kOrbHItems];
+    uint32_t hit[kOrbHItems];  // per item: LDS byte address of its source dwords | of its H slot << 16
 #pragma unroll
     for (int k = 0; k < kOrbHItems; ++k) hit[k] = tab[lane + 64 * k];
     // wave -> (level, first keypoint) from the level capacities (host constants)
@@ -2139,6 +2140,13 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * Lh), &bias);
     uint32_t* src = s_src[wid];
     uint32_t* hb = s_h[wid];
+    {
+        typedef __attribute__((address_space(3))) uint32_t lds_w32;
+        const uint32_t src_a = (uint32_t)(uintptr_t)(lds_w32*)src, hb_a = (uint32_t)(uintptr_t)(lds_w32*)hb;
+#pragma unroll
+        for (int k = 0; k < kOrbHItems; ++k)
+            hit[k] = (src_a + 4u * (hit[k] & 0xFFFFu)) | ((hb_a + 16u * (hit[k] >> 16)) << 16);
+    }
     if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
 #pragma unroll
     for (int k = 0; k < (64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES); ++k) {
@@ -2251,10 +2259,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
 #else
         constexpr int kHRun = kOrbHItems;
 #endif
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < kHRun; ++k) {
-            if (hit[k] != ~0u) {
-                const uint32_t* q = src + (hit[k] & 0xFFFFu);
+            {  // lanes without an item run the dummy one (orb_tables)
+                typedef __attribute__((address_space(3))) uint32_t lds_w32;
+                const lds_w32* q = (const lds_w32*)(uintptr_t)(hit[k] & 0xFFFFu);
                 uint32_t h[2][4];
 #pragma unroll
                 for (int rr = 0; rr < 2; ++rr) {
@@ -2276,8 +2285,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 }
                 // (row 2p, row 2p + 1) as u16 pairs: one v_perm each (the sums are < 2^16)
                 auto pk = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
-                *(uint4*)(hb + 4 * (hit[k] >> 16)) = uint4{pk(h[0][0], h[1][0]), pk(h[0][1], h[1][1]),
-                                                          pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(hit[k] >> 16) =
+                    u32x4{pk(h[0][0], h[1][0]), pk(h[0][1], h[1][1]), pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
             }
         }
 #if defined(ORBFE_X_NOCENT)  // experiment: no centroid / angle, wrong angles and bits
