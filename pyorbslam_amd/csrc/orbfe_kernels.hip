@@ -2337,7 +2337,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 const df2 mm = (df2){py, py} * (df2){a, -b};
                 const df2 rc = __builtin_elementwise_fma((df2){px, px}, (df2){b, a}, mm) + (df2){12582912.0f, 12582912.0f};
                 const uint32_t xb = __float_as_uint(rc.x), yb = __float_as_uint(rc.y);
-                const uint32_t addr = ((xb >> 1) & 0xFFFFFFu) * (uint32_t)(4 * kHDw) + ((yb << 2) + kc);
+                // v_mad_u32_u24 over a v_lshl_add (the compiler's v_mul_u32_u24 + v_lshlrev + v_add3 is one more)
+                static_assert(4 * kHDw == 0xA0, "H row-pair stride of the v_mad_u32_u24 operand");
+                uint32_t addr;
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(addr) : "v"(xb >> 1), "s"(0xA0u), "v"((yb << 2) + kc));
 #if defined(ORBFE_X_NOCONF)  // experiment (tools/dbg/build_variant.sh): conflict-free reads, wrong bits
                 lds_u32* p = (lds_u32*)(uintptr_t)((uint32_t)(uintptr_t)(lds_u32*)hb + 4 * (lane & 31) + (addr & 0x40));
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
