@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 // and 64-bit store address are gone).  Blocks of 256 <= 64 W_g R_s <= 512 threads (the host picks R_s).
 __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                      uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
-                                                     const ResizeY* __restrict__ yt, int wg) {
+                                                     const ResizeY* __restrict__ yt, int wg, int remw) {
     set_prio(g, kPrioResize);
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     uint32_t* s_src = (uint32_t*)rs_lds;  // staged source rows
@@ -331,9 +331,17 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
     const uint32_t src_lds = (uint32_t)(uintptr_t)(lds_u32*)s_src;
     // this thread's group: x selectors / weights straight from the table (issued with the staging loads)
-    const int wv = t >> 6, set = __builtin_amdgcn_readfirstlane(wv / wg), nset = nthr / (64 * wg);
-    const int grp = (wv - set * wg) * 64 + (t & 63);
-    const bool own = grp < ngrp;
+    // remw = 1: the last wave takes the groups past the wg full 64-group chunks (rem < 64 of them) for all
+    // rows of the band: lane j owns group wg * 64 + j % rem and rows j / rem, + 64 / rem, ... (a per-lane
+    // row), instead of a mostly idle row-uniform wave per row
+    const int wv = t >> 6, fullw = (nthr >> 6) - remw, nset = fullw / wg;
+    const bool remwave = wv >= fullw;
+    const int set = __builtin_amdgcn_readfirstlane(remwave ? 0 : wv / wg);
+    const int rem = ngrp - wg * 64, lane = t & 63;
+    const int rstep = remwave ? 64 / rem : nset;  // rows between a lane's rows in the remainder wave
+    const int grp = remwave ? wg * 64 + lane % rem : (wv - set * wg) * 64 + lane;
+    const int row0 = remwave ? lane / rem : set;
+    const bool own = remwave ? lane < rstep * rem : grp < ngrp;
     uint4 e{}, aa{};
     int sx0 = 0;
     if (own) {
@@ -367,8 +375,8 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     const int dx = 4 * grp;
     const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
     const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-    for (int rr = set; rr < nrow; rr += nset) {
-        const ResizeY y = yb[rr];  // uniform: scalar loads
+    auto row = [&](int rr) {
+        const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
         const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
         const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
         auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
@@ -399,6 +407,11 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         // pixels past L.w land in the row's pitch padding
         __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
                                               (uint32_t)(rr * L.pitch), 0);
+    };
+    if (!remwave) {
+        for (int rr = set; rr < nrow; rr += nset) row(rr);
+    } else {
+        for (int rr = row0; rr < nrow; rr += rstep) row(rr);
     }
 }
 
@@ -2846,11 +2859,19 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
     // production: k_resize_rows (profiles/r03/resize_rows_ab_r3f.log: 414 -> 394 us per 256 pairs
     // standalone, +0.8 % on the 4-handle step); variants (tools/microbench.py): 4 = the item-mapped
     // k_resize, 1 / 2 = its staging-only / compute-only ablations
-    if (variant == 0 || variant == 3) {
-        const int ngrp = (L.w + 3) / 4, wg = (ngrp + 63) / 64;
-        const int sets = (4 + wg - 1) / wg;  // row sets: >= 256 threads per block (the staging threads)
-        hipLaunchKernelGGL(k_resize_rows, grid, dim3(64 * wg * sets), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in,
-                           in_pitch, ws, xt, yt, wg);
+    if (variant == 0 || variant == 3 || variant == 5) {
+        // a level whose groups leave a last chunk of fewer than 40 (of 64) takes it in one remainder wave
+        // (variant 5 / ORBFE_RS_REM=0: never, every chunk row-uniform)
+        static const int rs_rem = [] {
+            const char* e = std::getenv("ORBFE_RS_REM");
+            return e ? std::atoi(e) : 1;
+        }();
+        const int ngrp = (L.w + 3) / 4, rem = ngrp % 64;
+        const int remw = (variant != 5 && rs_rem != 0 && ngrp >= 64 && rem > 0 && rem < 40) ? 1 : 0;
+        const int wg = remw ? ngrp / 64 : (ngrp + 63) / 64;
+        const int sets = std::max(1, (4 - remw + wg - 1) / wg);  // >= 256 threads per block (the staging threads)
+        hipLaunchKernelGGL(k_resize_rows, grid, dim3(64 * (wg * sets + remw)), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g,
+                           l, in, in_pitch, ws, xt, yt, wg, remw);
         return hipGetLastError();
     }
     const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
