@@ -23,10 +23,11 @@ pyorbslam_amd/_lib/%.o: pyorbslam_amd/csrc/%.cpp $(HDR)
 	@mkdir -p pyorbslam_amd/_lib
 	$(HIPCC) -O3 -std=c++17 -fPIC -Wall -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c -o $@ $<
 
-# orbfe_build_id(): the hash of every source and header, regenerated whenever the library is relinked
+# orbfe_build_id(): the hash of every source and header and of the compiler flags (a variant build with
+# extra -D switches gets its own id), regenerated whenever the library is relinked
 BUILD_ID_O := pyorbslam_amd/_lib/build_id.o
 $(LIB): $(OBJ)
-	@printf 'const char* orbfe_build_id(void) { return "%s"; }\n' "$$(cat $(SRC) $(CSRC) $(HDR) | sha256sum | cut -c1-16)" \
+	@printf 'const char* orbfe_build_id(void) { return "%s"; }\n' "$$( (cat $(SRC) $(CSRC) $(HDR); echo '$(HIPFLAGS)') | sha256sum | cut -c1-16)" \
 	  > pyorbslam_amd/_lib/build_id.c
 	gcc -O2 -fPIC -c -o $(BUILD_ID_O) pyorbslam_amd/_lib/build_id.c
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) $(BUILD_ID_O) -lz -lpthread

@@ -178,7 +178,7 @@ def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, pro
 
 
 # ------------------------------------------------------------------------------------------ parity check
-def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64):
+def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64, camera=None):
     """About `pairs_total` pairs of the timed batch (per handle: its first and last pair and evenly spaced
     ones between) against the oracle extractor and the stereo restatement, bit for bit; every handle's
     overflow word.  The device results are fetched first; the oracle runs on a thread pool (its C calls
@@ -186,8 +186,9 @@ def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64):
     from concurrent.futures import ThreadPoolExecutor
     from oracle import stereo_oracle
     from oracle.oracle import OracleExtractor
-    from pyorbslam_amd.batch import KITTI_BF, KITTI_FX
+    from pyorbslam_amd.batch import camera_constants
     from pyorbslam_amd.frame import to_reference_lists
+    bf, fx = camera or camera_constants(width, height)
     ovf, jobs = 0, []
     per = max(2, -(-pairs_total // max(len(fes), 1)))
     first = 0
@@ -208,9 +209,9 @@ def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64):
         if gk.tobytes() != kl.tobytes() or not np.array_equal(gd, dl) or hk.tobytes() != kr.tobytes() \
                 or not np.array_equal(hd, dr):
             return f"handle {hi} pair {p}: extraction differs from the oracle"
-        u, d = to_reference_lists(res, gk, KITTI_BF)
+        u, d = to_reference_lists(res, gk, bf)
         ou, od, _ = stereo_oracle.compute_stereo_matches(kl, kr, dl, dr, oL.sheared_pyramid(), oR.sheared_pyramid(),
-                                                         t["scale"], t["inv_scale"], KITTI_BF, np.float32(KITTI_FX))
+                                                         t["scale"], t["inv_scale"], bf, np.float32(fx))
         for a, b in ((u, ou), (d, od)):
             sa, va = stereo_oracle.encode(a)
             sb, vb = stereo_oracle.encode(b)
@@ -352,9 +353,10 @@ class Shard:
     whole front-end on its own stream so that the latency-bound stages of one overlap the issue-bound
     stages of another; every pair is processed exactly once per step."""
 
-    def __init__(self, images, n_pairs, streams, dev, width, height, nfeatures, lanes=1):
+    def __init__(self, images, n_pairs, streams, dev, width, height, nfeatures, lanes=1, camera=None):
         import torch
-        from pyorbslam_amd.batch import StereoFrontEnd
+        from pyorbslam_amd.batch import StereoFrontEnd, camera_constants
+        self.bf, self.fx = camera or camera_constants(width, height)
         S = max(1, min(streams, n_pairs))
         self.counts = [shard(n_pairs, S, i)[1] for i in range(S)]
         self.fes = [StereoFrontEnd(width, height, max_pairs=max(c, 1), nfeatures=nfeatures, lanes=lanes)
@@ -367,10 +369,9 @@ class Shard:
         self.n_pairs = n_pairs
 
     def step(self, subs=None):
-        from pyorbslam_amd.batch import KITTI_BF, KITTI_FX
         for f, st, sub, c in zip(self.fes, self.streams, subs or self.subs, self.counts):
             if c:
-                f.enqueue(sub, c, KITTI_BF, KITTI_FX, stream_ptr=st.cuda_stream)
+                f.enqueue(sub, c, self.bf, self.fx, stream_ptr=st.cuda_stream)
 
 
 def timed(fn, steps, warmup, dev, world):
@@ -440,7 +441,7 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
             st.wait_event(ev["in"][b][j])
             if seen[b]:
                 st.wait_event(ev["out"][b][j])         # drec[b] rows of handle j have left the device
-            f.enqueue(dbuf[b][2 * o0:2 * o1], c, stream_ptr=st.cuda_stream)
+            f.enqueue(dbuf[b][2 * o0:2 * o1], c, sh.bf, sh.fx, stream_ptr=st.cuda_stream)
             call("orbfe_batch_pack_device", f.handle, C.c_void_p(drec[b][o0].data_ptr()), rb, 0, c,
                  C.c_void_p(st.cuda_stream))
             ev["free"][b][j].record(st)
@@ -489,6 +490,136 @@ def stamped(name: str, key: str, build: str):
     return data[key], f"profiles/{name} {key} (build {build}, git {meta.get('git_rev', '?')})"
 
 
+# ----------------------------------------------------------------------------- standalone pass / roofline
+def standalone_stages(images, P, width, height, nfeatures, steps, dev) -> dict:
+    """The P pairs as ONE handle on ONE stream (stream path: profiling events between the stages), mean ms
+    per stage over `steps` batches."""
+    import torch
+    from pyorbslam_amd._lib import call
+    from pyorbslam_amd.batch import StereoFrontEnd, camera_constants
+    bf, fx = camera_constants(width, height)
+    torch.cuda.synchronize(dev)
+    solo = StereoFrontEnd(width, height, max_pairs=P, nfeatures=nfeatures, lanes=1)
+    st0 = torch.cuda.current_stream(dev)
+    for _ in range(2):
+        solo.enqueue(images, P, bf, fx, stream_ptr=st0.cuda_stream)
+    torch.cuda.synchronize(dev)
+    call("orbfe_profile_begin", solo.handle, steps)
+    for _ in range(steps):
+        solo.enqueue(images, P, bf, fx, stream_ptr=st0.cuda_stream)
+    ms = (C.c_float * len(STAGES))()
+    nb = C.c_int32()
+    call("orbfe_profile_read", solo.handle, ms, C.byref(nb))
+    del solo
+    return {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
+
+
+def roofline_block(stage_ms: dict, P: int, width: int, height: int, nfeatures: int, workload: str, build: str,
+                   pairs_per_s_per_gpu, steps: int) -> dict:
+    """roofline (the largest standalone stage against HBM), stage_roofline, valu_roofline: PMC figures only
+    from profiles/*.json entries stamped with the loaded library's build id."""
+    out = {}
+    total_b, per_stage_b = algorithmic_bytes_per_pair(width, height, nfeatures)
+    tr, tr_src = stamped("traffic.json", workload + "_standalone", build)
+    dom = max(stage_ms, key=stage_ms.get)
+    ach = {s: per_stage_b[s] * P / (stage_ms[s] * 1e-3) / 1e9 for s in STAGES
+           if stage_ms[s] > 0 and per_stage_b[s] > 0}
+    out["stage_ms_standalone_step"] = {k: round(v, 4) for k, v in stage_ms.items()}
+    out["roofline"] = {
+        "bound": "hbm", "kernel": STAGE_KERNELS[dom], "stage": dom, "achieved": round(ach[dom], 3),
+        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach[dom] / HBM_PEAK_GBS, 6),
+        "traffic": (tr or {}).get(dom), "traffic_source": tr_src,
+        "measured": f"standalone pass: {P} pairs as one handle on one stream, HIP events around each stage, "
+                    f"mean of {steps} steps (rocprof trace: the {2 * P}-image dispatches)",
+        "algorithmic_bytes_per_pair": per_stage_b[dom], "pipeline_bytes_per_pair": total_b,
+        "pipeline_frac": (round(pairs_per_s_per_gpu * total_b / (HBM_PEAK_GBS * 1e9), 6)
+                          if pairs_per_s_per_gpu else None)}
+    out["stage_roofline"] = {s: {"ms": round(stage_ms[s], 4), "achieved_GBs": round(ach[s], 3),
+                                 "frac": round(ach[s] / HBM_PEAK_GBS, 6), "traffic": (tr or {}).get(s)}
+                             for s in ach}
+    # the bound these kernels actually meet: VALU issue (wave-instructions per step from SQ_INSTS_VALU over
+    # the same standalone pass, profiles/valu.json, tools/valu.py); busy-cycle counters beside it
+    vi, vi_src = stamped("valu.json", workload + "_standalone", build)
+    if vi:
+        inst = {k: v for k, v in vi.items() if k in STAGES}
+        vst = {s: inst[s] / (stage_ms[s] * 1e-3) / 1e9 for s in inst if stage_ms.get(s, 0) > 0}
+        vdom = max(vst, key=lambda s: stage_ms[s])
+        out["valu_roofline"] = {
+            "bound": "valu", "unit": "G wave-instructions/s", "peak": VALU_PEAK_GIPS,
+            "peak_def": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction of the packed-16-bit / "
+                        "dot / perm / sad / shift / multiply class; the add / logic / mov class issues at ~2.4 "
+                        f"cycles ({VALU_PEAK_FAST_CLASS_GIPS:.0f} G/s): a class-peak fraction, see busy",
+            "kernel": STAGE_KERNELS[vdom], "achieved": round(vst[vdom], 2),
+            "frac": round(vst[vdom] / VALU_PEAK_GIPS, 4),
+            "stages": {s: {"inst_per_step": int(inst[s]), "achieved": round(v, 2),
+                           "frac": round(v / VALU_PEAK_GIPS, 4)} for s, v in vst.items()},
+            "pipeline_frac": (round(sum(inst.values()) * pairs_per_s_per_gpu / P / 1e9 / VALU_PEAK_GIPS, 4)
+                              if pairs_per_s_per_gpu else None),
+            "source": vi_src + " (rocprofv3 --pmc SQ_INSTS_VALU)"}
+        if "busy" in vi:  # per-stage VALU-busy fraction from SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES (tools/valu.py)
+            out["valu_roofline"]["busy"] = vi["busy"]
+    else:
+        out["valu_roofline"] = {"dropped": vi_src}
+    return out
+
+
+def workload_name(width, height, nfeatures, P, total_pairs=0):
+    cam, _ = CAMERAS.get((width, height), ("custom", f"{width}x{height}"))
+    return f"{cam}{width}x{height}_synth_{nfeatures}f_" + (f"{total_pairs}pairs_total" if total_pairs else f"{P}pairs")
+
+
+def c5_euroc(args, dev) -> dict:
+    """BASELINE configs[4]: EuRoC 752x480, 1000 features, 512 pairs per step on this GPU (the default bench
+    step's handles and streams), timed like the headline; its own parity sample (64 pairs against the
+    oracle) and its standalone per-stage roofline from the build-stamped EuRoC PMC entries."""
+    import torch
+    from pyorbslam_amd import synth
+    W, H, N, P = 752, 480, 1000, args.pairs
+    host = synth.make_batch(P, seed0=0, width=W, height=H)
+    images = torch.from_numpy(host).to(dev)
+    sh = Shard(images, P, args.streams, dev, W, H, N, args.lanes)
+    el = timed(sh.step, args.steps, args.warmup, dev, 1)
+    checked, ovf, bad = parity_check(sh.fes, sh.counts, host, W, H, N, args.parity_pairs)
+    pps = P * args.steps / el
+    wl = workload_name(W, H, N, P)
+    out = {"value": round(pps, 2), "unit": "pairs/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "steps": args.steps, "warmup": args.warmup, "workload": wl, "pairs_per_step": P, "nfeatures": N,
+           "handles": len(sh.fes), "parity_checked_pairs": checked, "overflow": ovf, "parity_failures": len(bad)}
+    del sh
+    if args.roofline_steps > 0:
+        stage_ms = standalone_stages(images, P, W, H, N, args.roofline_steps, dev)
+        from pyorbslam_amd import _lib
+        out.update(roofline_block(stage_ms, P, W, H, N, wl, _lib.build_id(), pps, args.roofline_steps))
+    if bad or ovf:
+        out["details"] = bad[:5]
+    return out
+
+
+def c4_rank_share(args, dev, c4_value) -> dict:
+    """One rank's share of 8-way C4 (BASELINE configs[3]: 64 pairs over 8 GPUs = 8 pairs per GPU) on this GPU,
+    timed like a step; the projected 8-GPU C4 rate is 64 pairs per rank-share step, and its efficiency
+    against 8 x this GPU's whole-C4 rate (c4_strong) says what the small shard costs."""
+    import torch
+    from pyorbslam_amd import synth
+    first, n = shard(C4_TOTAL_PAIRS, 8, 0)
+    host = synth.make_batch(n, seed0=first, width=args.width, height=args.height)
+    images = torch.from_numpy(host).to(dev)
+    sh = Shard(images, n, args.streams, dev, args.width, args.height, args.nfeatures, args.lanes)
+    el = timed(sh.step, max(args.steps, 50), args.warmup, dev, 1)
+    steps = max(args.steps, 50)
+    ms = el / steps * 1e3
+    checked, ovf, bad = parity_check(sh.fes, sh.counts, host, args.width, args.height, args.nfeatures, n)
+    proj = C4_TOTAL_PAIRS / (ms * 1e-3)
+    return {"pairs": n, "handles": len(sh.fes), "steps": steps, "ms_per_step": round(ms, 4),
+            "value": round(n / (ms * 1e-3), 2), "unit": "pairs/s",
+            "projected_8gpu_c4_pairs_per_s": round(proj, 1),
+            "projected_8way_efficiency": round(proj / (8 * c4_value), 4) if c4_value else None,
+            "graphs": all(f.graph_stats()["launches"] > 0 for f in sh.fes),
+            "parity_checked_pairs": checked, "parity_failures": len(bad), "overflow": ovf,
+            "what": "8 pairs (one rank's share of 64 over 8 GPUs) on this GPU, timed like a step; projected 8-way "
+                    "C4 rate = 64 / rank-share step time, efficiency = that / (8 x c4_strong.value)"}
+
+
 # --------------------------------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -520,6 +651,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (64 pairs in total) line")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed (PCIe-inclusive) line")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 tracking-loop latency (N = 1)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 EuRoC line (N = 1, KITTI runs only)")
     args = ap.parse_args()
 
     wr = check_world(args)
@@ -554,8 +686,6 @@ def main():
 
     from pyorbslam_amd import _lib, synth
     from pyorbslam_amd import dist as D
-    from pyorbslam_amd._lib import call
-    from pyorbslam_amd.batch import StereoFrontEnd, KITTI_BF, KITTI_FX
 
     strong = args.total_pairs > 0
     if strong:
@@ -618,24 +748,22 @@ def main():
     if extras and not args.no_host_fed:
         hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2)
 
+    # ---- C4's rank share (8 pairs) on this GPU, and C5 (EuRoC), N = 1
+    share = None
+    if extras and world == 1 and not strong and not args.no_c4:
+        share = c4_rank_share(args, dev, c4["value"] if c4 else None)
+    c5 = None
+    if extras and world == 1 and not strong and not args.no_c5 and (args.width, args.height) == (1241, 376):
+        c5 = c5_euroc(args, dev)
+        if c5["parity_failures"] or c5["overflow"]:
+            print(json.dumps({"error": "C5 (EuRoC) workload failed its parity check", **c5}), flush=True)
+            raise SystemExit(3)
+
     # ---- standalone per-stage pass: the same P pairs as one handle on one stream, HIP events per stage
     stage_ms = {}
     if args.roofline_steps > 0 and rank == 0:
         del sh
-        torch.cuda.synchronize(dev)
-        solo = StereoFrontEnd(args.width, args.height, max_pairs=P, nfeatures=args.nfeatures, lanes=1)
-        st0 = torch.cuda.current_stream(dev)
-        for _ in range(2):
-            solo.enqueue(images, P, KITTI_BF, KITTI_FX, stream_ptr=st0.cuda_stream)
-        torch.cuda.synchronize(dev)
-        call("orbfe_profile_begin", solo.handle, args.roofline_steps)
-        for _ in range(args.roofline_steps):
-            solo.enqueue(images, P, KITTI_BF, KITTI_FX, stream_ptr=st0.cuda_stream)
-        ms = (C.c_float * len(STAGES))()
-        nb = C.c_int32()
-        call("orbfe_profile_read", solo.handle, ms, C.byref(nb))
-        stage_ms = {s: ms[i] / max(nb.value, 1) for i, s in enumerate(STAGES)}
-        del solo
+        stage_ms = standalone_stages(images, P, args.width, args.height, args.nfeatures, args.roofline_steps, dev)
 
     c3 = None
     if extras and world == 1 and not args.no_c3 and (ROOT / "tests" / "golden" / "sequence_kitti_synth.npz").exists():
@@ -646,10 +774,8 @@ def main():
 
     if rank == 0:
         build = _lib.build_id()
-        total_b, per_stage_b = algorithmic_bytes_per_pair(args.width, args.height, args.nfeatures)
         cam, cam_name = CAMERAS.get((args.width, args.height), ("custom", f"{args.width}x{args.height}"))
-        workload = (f"{cam}{args.width}x{args.height}_synth_{args.nfeatures}f_"
-                    + (f"{args.total_pairs}pairs_total" if strong else f"{P}pairs"))
+        workload = workload_name(args.width, args.height, args.nfeatures, P, args.total_pairs if strong else 0)
         out = {"metric": f"stereo pairs/s (ORB extract L+R + stereo match), {cam_name}, 1/2/4/8 GPU"}
         if elapsed is not None:
             pairs_per_s = total * args.steps / elapsed
@@ -673,47 +799,16 @@ def main():
         if parity is not None:
             out.update(parity)
         if stage_ms:
-            tr, tr_src = stamped("traffic.json", workload + "_standalone", build)
-            dom = max(stage_ms, key=stage_ms.get)
-            ach = {s: per_stage_b[s] * P / (stage_ms[s] * 1e-3) / 1e9 for s in STAGES
-                   if stage_ms[s] > 0 and per_stage_b[s] > 0}
-            out["stage_ms_standalone_step"] = {k: round(v, 4) for k, v in stage_ms.items()}
-            out["roofline"] = {
-                "bound": "hbm", "kernel": STAGE_KERNELS[dom], "stage": dom, "achieved": round(ach[dom], 3),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach[dom] / HBM_PEAK_GBS, 6),
-                "traffic": (tr or {}).get(dom), "traffic_source": tr_src,
-                "measured": f"standalone pass: {P} pairs as one handle on one stream, HIP events around each stage, "
-                            f"mean of {args.roofline_steps} steps (rocprof trace: the {2 * P}-image dispatches)",
-                "algorithmic_bytes_per_pair": per_stage_b[dom], "pipeline_bytes_per_pair": total_b,
-                "pipeline_frac": (round(pairs_per_s / world * total_b / (HBM_PEAK_GBS * 1e9), 6)
-                                  if pairs_per_s else None)}
-            out["stage_roofline"] = {s: {"ms": round(stage_ms[s], 4), "achieved_GBs": round(ach[s], 3),
-                                         "frac": round(ach[s] / HBM_PEAK_GBS, 6), "traffic": (tr or {}).get(s)}
-                                     for s in ach}
-            # the bound these kernels actually meet: VALU issue (wave-instructions per step from
-            # SQ_INSTS_VALU over the same standalone pass, profiles/valu.json, tools/valu.py)
-            vi, vi_src = stamped("valu.json", workload + "_standalone", build)
-            if vi:
-                vst = {s: vi[s] / (stage_ms[s] * 1e-3) / 1e9 for s in vi if stage_ms.get(s, 0) > 0}
-                vdom = max(vst, key=lambda s: stage_ms[s])
-                out["valu_roofline"] = {
-                    "bound": "valu", "unit": "G wave-instructions/s", "peak": VALU_PEAK_GIPS,
-                    "peak_def": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction of the packed-16-bit / "
-                                "dot / perm / sad / shift / multiply class (profiles/r03/mulrate_r3b.log); the "
-                                f"add / logic / mov class issues at ~2.4 cycles ({VALU_PEAK_FAST_CLASS_GIPS:.0f} G/s)",
-                    "kernel": STAGE_KERNELS[vdom], "achieved": round(vst[vdom], 2),
-                    "frac": round(vst[vdom] / VALU_PEAK_GIPS, 4),
-                    "stages": {s: {"inst_per_step": int(vi[s]), "achieved": round(v, 2),
-                                   "frac": round(v / VALU_PEAK_GIPS, 4)} for s, v in vst.items()},
-                    "pipeline_frac": (round(sum(vi.values()) * pairs_per_s / world / P / 1e9 / VALU_PEAK_GIPS, 4)
-                                      if pairs_per_s else None),
-                    "source": vi_src + " (rocprofv3 --pmc SQ_INSTS_VALU)"}
-            else:
-                out["valu_roofline"] = {"dropped": vi_src}
+            out.update(roofline_block(stage_ms, P, args.width, args.height, args.nfeatures, workload, build,
+                                      pairs_per_s / world if pairs_per_s else None, args.roofline_steps))
         if gather is not None:
             out["with_gather"] = gather
         if c4 is not None:
             out["c4_strong"] = c4
+        if share is not None:
+            out["c4_rank_share"] = share
+        if c5 is not None:
+            out["c5_euroc"] = c5
         if hf is not None:
             out["host_fed"] = hf
         if c3 is not None:

@@ -29,6 +29,12 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header (orbfe_abi_version() returns the library's).  4: ORBFE_NSTAGES = 5 (stage 3
+ * describe, 4 stereo; the round-1 blur stage and orbfe_set_blur_fork are gone), orbfe_set_graphs,
+ * orbfe_set_octree_kernel / orbfe_get_octree_kernel, orbfe_debug_detect_stats. */
+#define ORBFE_ABI_VERSION 4
+int32_t orbfe_abi_version(void);
+
 #define ORBFE_OK 0
 #define ORBFE_EINVAL (-1)    /* bad argument / unsupported configuration            */
 #define ORBFE_ENOMEM (-2)    /* host or device allocation failed                    */
@@ -170,6 +176,15 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
  * their layout do not depend on it. */
 int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
 
+/* orbfe_set_graphs: 1 (default) = orbfe_frontend_batch_device (one lane) and orbfe_frame_extract run their
+ * whole enqueue (12-16 kernels, memsets and copies) as a HIP graph, captured on the first call with a given
+ * (buffers, pointers, sizes, bf, fx) key and replayed with one hipGraphLaunch afterwards (up to 8 cached
+ * graphs per handle, dropped when the handle's buffers are reallocated); 0 = launch every operation on the
+ * stream.  Results do not depend on it.  Profiling (orbfe_profile_begin) always takes the stream path.
+ * orbfe_graph_stats: captures and graph launches so far, graphs cached now (any pointer may be NULL). */
+int orbfe_set_graphs(orbfe_handle h, int32_t on);
+int orbfe_graph_stats(orbfe_handle h, int64_t* captures, int64_t* launches, int32_t* cached);
+
 /* Device result layout of the last batch (pointers into handle-owned device memory):
  *   kps   : n_images x cap  orbfe_keypoint   (cap = *kp_cap)
  *   desc  : n_images x cap x 32 u8
@@ -306,6 +321,18 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
 /* orbfe_debug_octree_profile: re-runs the last batch's octree stage with wall-clock marks (100 MHz ticks,
  * 64 per (image, level), 0 = not reached) written by each workgroup's first thread; development aid. */
 int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n);
+/* orbfe_debug_detect_stats: re-runs the last batch's FAST cell stage (idempotent) with counters:
+ * stats[0] = cells processed, stats[1] = cells whose iniTh / minTh queues met so that the cell took the
+ * one-pass path (both thresholds over the minTh queue), stats[2] = cells that fell back to minTh
+ * (ORBextractor.cpp:811-815) on the two-queue path.  Development aid; results are unchanged. */
+int orbfe_debug_detect_stats(orbfe_handle h, int64_t* stats);
+
+/* DistributeOctTree implementation (ORBextractor.cpp:539-762; results are identical): 0 = automatic
+ * (k_octree_bins, or the per-candidate k_octree when the bins' LDS carve would exceed 150 KiB), 1 = always
+ * the per-candidate k_octree.  orbfe_get_octree_kernel reports the reserved geometry's choice (0 bins,
+ * 1 per-candidate) and the bins kernel's LDS need. */
+int orbfe_set_octree_kernel(orbfe_handle h, int32_t kernel);
+int orbfe_get_octree_kernel(orbfe_handle h, int32_t* kernel, int64_t* bins_lds_bytes);
 
 /* ---- bag-of-words vocabulary (pyDBoW/TemplatedVocabulary.py) ---------------------------
  *

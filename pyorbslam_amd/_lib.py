@@ -96,6 +96,12 @@ SIGNATURES = {
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
     "orbfe_set_lanes": [C.c_void_p, C.c_int32],
+    "orbfe_abi_version": [],
+    "orbfe_set_graphs": [C.c_void_p, C.c_int32],
+    "orbfe_graph_stats": [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int32)],
+    "orbfe_set_octree_kernel": [C.c_void_p, C.c_int32],
+    "orbfe_get_octree_kernel": [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)],
+    "orbfe_debug_detect_stats": [C.c_void_p, C.POINTER(C.c_int64)],
     "orbfe_vocab_load_text": [C.c_char_p, C.POINTER(C.c_void_p)],
     "orbfe_vocab_create": [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_void_p, C.POINTER(C.c_void_p)],

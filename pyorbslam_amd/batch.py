@@ -16,12 +16,21 @@ from ._lib import KP_DTYPE, BatchView, call, ptr
 
 KITTI_BF = 386.1448  # KITTI00-02.yaml Camera.bf
 KITTI_FX = 718.856   # KITTI00-02.yaml Camera.fx
+# EuRoC MAV rectified stereo (ORB-SLAM2 EuRoC.yaml Camera.bf, Camera.fx; the reference ships KITTI settings
+# only), the EuRoC case of tests/test_gpu_stereo.py
+EUROC_BF = 47.90639384423901
+EUROC_FX = 435.2046959714599
+
+
+def camera_constants(width: int, height: int) -> tuple[float, float]:
+    """(bf, fx) of the camera whose image size this is: EuRoC for 752x480, KITTI otherwise."""
+    return (EUROC_BF, EUROC_FX) if (int(width), int(height)) == (752, 480) else (KITTI_BF, KITTI_FX)
 
 
 class StereoFrontEnd:
     def __init__(self, width: int = 1241, height: int = 376, max_pairs: int = 64, nfeatures: int = 2000,
                  scaleFactor: float = 1.2, nlevels: int = 8, iniThFAST: int = 20, minThFAST: int = 7,
-                 resize_simd_lanes: int = 16, lanes: int = 4):
+                 resize_simd_lanes: int = 16, lanes: int = 4, graphs: bool = True):
         self.width, self.height, self.max_pairs = int(width), int(height), int(max_pairs)
         self._params = _lib.make_params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes)
         h = C.c_void_p()
@@ -30,6 +39,8 @@ class StereoFrontEnd:
         call("orbfe_batch_reserve", h, self.width, self.height, 2 * self.max_pairs)
         # concurrent chunks of enqueue() on internal streams (results are independent of it)
         call("orbfe_set_lanes", h, int(lanes))
+        # one-lane enqueues replay a captured HIP graph (orbfe_set_graphs; results do not depend on it)
+        call("orbfe_set_graphs", h, int(bool(graphs)))
         v = BatchView()
         call("orbfe_batch_view_get", h, C.byref(v))
         self.kp_cap = v.kp_cap
@@ -62,6 +73,12 @@ class StereoFrontEnd:
         n = images.shape[0] if n_images is None else int(n_images)
         call("orbfe_extract_batch_device", self._h, C.c_void_p(images.data_ptr()), self.width * self.height, n,
              C.c_void_p(stream_ptr))
+
+    def graph_stats(self) -> dict:
+        """HIP-graph captures and launches of this handle so far, and the graphs cached now."""
+        cap, lau, n = C.c_int64(), C.c_int64(), C.c_int32()
+        call("orbfe_graph_stats", self._h, C.byref(cap), C.byref(lau), C.byref(n))
+        return {"captures": cap.value, "launches": lau.value, "cached": n.value}
 
     def overflow(self) -> int:
         """Overflow word of the last batch (0 = no on-device capacity bound was hit); synchronises."""

@@ -76,9 +76,6 @@ struct ResizeY {
     int16_t b0, b1;
 };
 
-// Kernels of the pipeline, indexing Geo::prio.
-enum { kPrioResize = 0, kPrioDetect, kPrioOctree, kPrioOrb, kPrioBucket, kPrioStereo, kPrioN };
-
 // Per-geometry constants passed by value to every kernel.
 struct Geo {
     int nlevels;
@@ -106,8 +103,8 @@ struct Geo {
     int oct_bins_max;    // k_octree (bins): most bins of any level
     int oct_tab_max;     // k_octree (bins): most X + Y table words of any level
     int oct_kblk_max;    // k_octree (bins): most 64-key blocks of any level (key_cap / 64 + 1)
-    int oct_v;           // k_octree implementation: 0 bins (default), 1 the per-candidate pass kernel (ORBFE_OCT_V)
-    int prio[8];         // wave issue priority (s_setprio) per kernel, kPrio* below; 0 = default (ORBFE_PRIO)
+    int oct_v;           // k_octree implementation: 0 bins (default), 1 the per-candidate pass kernel (automatic
+                         // when the bins' LDS would exceed 150 KiB, or orbfe_set_octree_kernel)
     int umax[16];
     float scale[kMaxLevels];
     float inv_scale[kMaxLevels];

@@ -95,10 +95,20 @@ struct orbfe_ctx {
     bool prof_on = false;
 
     hipStream_t own_stream = nullptr;
-    // ORBFE_STAGE_REPEAT=r,d,o,k,s (development aid): launches of each stage per batch (default 1 each).
-    // Every stage is idempotent, so a second launch measures the stage's marginal cost inside the
-    // concurrent multi-handle step, where its standalone time says little.
-    int stage_rep[ORBFE_NSTAGES] = {1, 1, 1, 1, 1};
+    bool octree_force = false;  // orbfe_set_octree_kernel(h, 1): the per-candidate k_octree at every geometry
+    // HIP graphs (orbfe_set_graphs, default on): a batch's or a frame's whole enqueue is captured once per
+    // (buffers, arguments) key into an executable graph and replayed with one hipGraphLaunch.  gen counts the
+    // reallocations of the handle's buffers / geometry changes, which every key includes; a capture goes on
+    // cap_stream, so the caller's stream only ever sees the launches.
+    bool use_graphs = true;
+    uint64_t gen = 0;
+    hipStream_t cap_stream = nullptr;
+    struct GraphEntry {
+        std::vector<uint64_t> key;
+        hipGraphExec_t exec;
+    };
+    std::vector<GraphEntry> graphs;
+    int64_t graph_launches = 0, graph_captures = 0;
     // orbfe_frontend_batch_device: up to kLanes concurrent chunks of the batch on internal streams
     int lanes = kLanes;  // orbfe_set_lanes
     hipStream_t lane_stream[kLanes] = {};
@@ -124,7 +134,14 @@ struct orbfe_ctx {
     size_t fo_count = 0, fo_kps = 0, fo_desc = 0, fo_uR = 0, fo_depth = 0, fo_status = 0, fo_match = 0, fo_ovf = 0,
            fo_shear = 0;
 
+    void drop_graphs() {
+        for (GraphEntry& e : graphs) (void)hipGraphExecDestroy(e.exec);
+        graphs.clear();
+        ++gen;
+    }
     ~orbfe_ctx() {
+        for (GraphEntry& e : graphs) (void)hipGraphExecDestroy(e.exec);
+        if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
         for (int k = 0; k < kLanes; ++k) {
@@ -460,19 +477,12 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.slot_total = std::max<int64_t>(slot_off, 1);
     g.key_total = std::max(key_off, 1);
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
-    // candidates in LDS when the node arrays leave room for them, else they stay in the global scratch
-    // (very large per-level feature counts, e.g. one level with thousands of features)
-    // ORBFE_PRIO=r,d,o,k,b,s: s_setprio level (0..3) of resize, detect, octree, k_orb, stereo bucket,
-    // k_stereo (tuning knob for the 4-stream step; default all 0)
-    if (const char* e = std::getenv("ORBFE_OCT_V")) g.oct_v = std::atoi(e) == 1 ? 1 : 0;
+    // octree kernel: k_octree_bins unless its LDS carve exceeds 150 KiB (or the caller forces the
+    // per-candidate k_octree, orbfe_set_octree_kernel); k_octree keeps the candidates in LDS when the node
+    // arrays leave room for them, else in the global scratch (very large per-level feature counts)
+    g.oct_v = c.octree_force ? 1 : 0;
     if (g.oct_v == 0 && octree_bins_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_v = 1;
-    if (const char* e = std::getenv("ORBFE_PRIO")) {
-        int k = 0;
-        for (const char* q = e; *q && k < kPrioN; ++q)
-            if (*q >= '0' && *q <= '3') g.prio[k++] = *q - '0';
-    }
     g.oct_keys = kOctKeys;
-    if (const char* e = std::getenv("ORBFE_OCT_KEYS")) g.oct_keys = std::max(0, std::min(kOctKeys, std::atoi(e)));
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024) g.oct_keys = 0;
     if (octree_lds_bytes(g, c.maxcell) > 150 * 1024)
         throw Error(ORBFE_EINVAL, "octree LDS footprint exceeds the 160 KiB LDS of a CU (nfeatures per level too large)");
@@ -541,10 +551,15 @@ void invalidate_results(orbfe_ctx& c) {
     c.frame_pyr = false;
 }
 
+// Per-kernel attributes (dynamic LDS above 64 KiB) are set here, when the geometry is built, and never
+// inside an enqueue: a graph capture (orbfe_set_graphs) records only stream work.
+void prepare_kernels(orbfe_ctx& c) { HIPCK(prepare_octree(c.geo, c.maxcell)); }
+
 void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     if (W <= 0 || H <= 0 || max_images <= 0) throw Error(ORBFE_EINVAL, "bad reserve geometry");
     if (W != c.W || H != c.H) {
         invalidate_results(c);
+        c.drop_graphs();
         build_geometry(c, W, H);
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
@@ -563,9 +578,11 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         c.d_octab.ensure(std::max<size_t>(c.octab.size(), 1));
         if (!c.octab.empty())
             HIPCK(hipMemcpy(c.d_octab.p, c.octab.data(), c.octab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        prepare_kernels(c);
     }
     if (max_images > c.max_images) {
         invalidate_results(c);  // the per-image buffers may move
+        c.drop_graphs();
         const Geo& g = c.geo;
         const size_t n = (size_t)max_images;
         c.d_ws.ensure(n * g.ws_bytes);
@@ -617,19 +634,15 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     uint8_t* desc = c.d_desc.p + (int64_t)i0 * g.kp_cap * 32;
     int* count = c.d_count.p + i0;
     if (prof) prof_mark(c, s, 0);
-    for (int r = 0; r < c.stage_rep[0]; ++r)
-        for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
+    for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
     if (prof) prof_mark(c, s, 1);
     (void)lane;
-    for (int r = 0; r < c.stage_rep[1]; ++r)
-        if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
+    if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
     if (prof) prof_mark(c, s, 2);
-    for (int r = 0; r < c.stage_rep[2]; ++r)
-        HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, c.d_octab.p, kd, kn, lvl_kp, lvl_count, c.d_overflow.p,
-                            c.maxcell, n, s));
+    HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, c.d_octab.p, kd, kn, lvl_kp, lvl_count, c.d_overflow.p,
+                        c.maxcell, n, s));
     if (prof) prof_mark(c, s, 3);
-    for (int r = 0; r < c.stage_rep[3]; ++r)
-        HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
+    HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
     if (prof) prof_mark(c, s, 4);
 }
 
@@ -692,7 +705,7 @@ void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int 
     a.out_stride = g.kp_cap;
     stereo_buffers(c, a, p0);
     stereo_consts(bf, fx, a);
-    for (int r = 0; r < c.stage_rep[4]; ++r) HIPCK(launch_stereo(g, a, n, s));
+    HIPCK(launch_stereo(g, a, n, s));
 }
 
 // Marks the end of a batch enqueue on s: orbfe_batch_pack_device orders its k_pack after it, whatever
@@ -715,6 +728,52 @@ void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStr
     record_batch_done(c, s);
 }
 
+constexpr size_t kMaxGraphs = 8;  // cached executable graphs per handle (e.g. two double-buffered inputs)
+
+uint64_t bits_of(double v) { uint64_t b; std::memcpy(&b, &v, 8); return b; }
+uint64_t bits_of(float v) { uint32_t b; std::memcpy(&b, &v, 4); return b; }
+uint64_t bits_of(const void* p) { return (uint64_t)(uintptr_t)p; }
+
+// Runs enqueue(stream) on s: directly, or (graphs on) as the executable graph cached under key — captured
+// on the first use of the key, replayed with one hipGraphLaunch afterwards.  Every pointer and argument
+// the enqueue bakes into its launches must be part of the key (c.gen stands for the handle's buffers).
+template <class F>
+void run_enqueue(orbfe_ctx& c, std::vector<uint64_t> key, hipStream_t s, F&& enqueue) {
+    if (!c.use_graphs || c.prof_on) {
+        enqueue(s);
+        return;
+    }
+    key.push_back(c.gen);
+    for (orbfe_ctx::GraphEntry& e : c.graphs)
+        if (e.key == key) {
+            HIPCK(hipGraphLaunch(e.exec, s));
+            ++c.graph_launches;
+            return;
+        }
+    if (!c.cap_stream) HIPCK(hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking));
+    hipGraph_t gr = nullptr;
+    HIPCK(hipStreamBeginCapture(c.cap_stream, hipStreamCaptureModeThreadLocal));
+    try {
+        enqueue(c.cap_stream);
+    } catch (...) {
+        if (hipStreamEndCapture(c.cap_stream, &gr) == hipSuccess && gr) (void)hipGraphDestroy(gr);
+        throw;
+    }
+    HIPCK(hipStreamEndCapture(c.cap_stream, &gr));
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    HIPCK(e);
+    if (c.graphs.size() >= kMaxGraphs) {
+        (void)hipGraphExecDestroy(c.graphs.front().exec);
+        c.graphs.erase(c.graphs.begin());
+    }
+    c.graphs.push_back({std::move(key), ex});
+    ++c.graph_captures;
+    HIPCK(hipGraphLaunch(ex, s));
+    ++c.graph_launches;
+}
+
 // The whole front-end for n_pairs pairs as up to kLanes concurrent chunks, each on its own internal
 // stream (fork from / join into the caller's stream with events): the latency-bound stages of one chunk
 // overlap the issue-bound stages of another.  Chunk 0 carries the profiling marks.
@@ -722,13 +781,17 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
                       hipStream_t s) {
     if (n_pairs <= 0) return;
     check_extract(c, pitch, 2 * n_pairs);
-    HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
     const int K = std::max(1, std::min(c.lanes, n_pairs));
     if (K == 1) {
-        extract_range(c, d_in, pitch, 0, 2 * n_pairs, s, true);
-        stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, s);
-        prof_mark(c, s, 5);
+        run_enqueue(c, {1, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx)}, s,
+                    [&](hipStream_t q) {
+                        HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), q));
+                        extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true);
+                        stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, q);
+                        prof_mark(c, q, 5);
+                    });
     } else {
+        HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
         if (!c.lane_stream[0]) {
             for (int k = 0; k < kLanes; ++k) {
                 HIPCK(hipStreamCreateWithFlags(&c.lane_stream[k], hipStreamNonBlocking));
@@ -764,12 +827,12 @@ hipStream_t own(orbfe_ctx& c) {
     return c.own_stream;
 }
 
+
 // Host image rows -> the pinned staging buffer (one CPU pass), then ONE contiguous host->device copy on s.
 // A hipMemcpy2DAsync straight from pageable memory is staged by the runtime row by row: 6.8 ms per pair
 // of 1241x376 images, against 0.4 ms for the whole pair call this way (tools/dbg/frame_extract_time.py).
 // The caller synchronises s before h_in is reused.
-void stage_images(orbfe_ctx& c, uint8_t* dst, const uint8_t* const* imgs, int n, int width, int height,
-                  int64_t stride, int64_t pitch, hipStream_t s) {
+void stage_host(orbfe_ctx& c, const uint8_t* const* imgs, int n, int width, int height, int64_t stride, int64_t pitch) {
     c.h_in.ensure((size_t)pitch * n);
     for (int i = 0; i < n; ++i) {
         uint8_t* o = c.h_in.p + (int64_t)i * pitch;
@@ -779,6 +842,11 @@ void stage_images(orbfe_ctx& c, uint8_t* dst, const uint8_t* const* imgs, int n,
             for (int y = 0; y < height; ++y) std::memcpy(o + (int64_t)y * width, imgs[i] + y * stride, width);
         }
     }
+}
+
+void stage_images(orbfe_ctx& c, uint8_t* dst, const uint8_t* const* imgs, int n, int width, int height,
+                  int64_t stride, int64_t pitch, hipStream_t s) {
+    stage_host(c, imgs, n, width, height, stride, pitch);
     HIPCK(hipMemcpyAsync(dst, c.h_in.p, (size_t)pitch * (n - 1) + (size_t)width * height, hipMemcpyHostToDevice, s));
 }
 
@@ -797,16 +865,13 @@ const char* orbfe_last_error(void) { return g_err.c_str(); }
 
 const char* orbfe_version(void) { return "orbfe 0.1 gfx950 (HIP, wave64, integer/bitwise, no MFMA)"; }
 
+int32_t orbfe_abi_version(void) { return ORBFE_ABI_VERSION; }
+
 int orbfe_create(const orbfe_params* params, orbfe_handle* out) {
     return guarded([&] {
         if (!params || !out) throw Error(ORBFE_EINVAL, "null argument");
         std::unique_ptr<orbfe_ctx> c(new orbfe_ctx());
         c->prm = *params;
-        if (const char* e = std::getenv("ORBFE_STAGE_REPEAT")) {
-            int k = 0;
-            for (const char* q = e; *q && k < ORBFE_NSTAGES; ++q)
-                if (*q >= '0' && *q <= '9') c->stage_rep[k++] = *q - '0';
-        }
         build_tables(*c);
         *out = c.release();
     });
@@ -926,27 +991,33 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
         hipStream_t s = own(*h);
         const int64_t pitch = ((int64_t)width * height + 255) & ~(int64_t)255;
         h->d_in.ensure(2 * (size_t)pitch);
+        if (want_pyramid) h->d_shear.ensure(2 * (size_t)g.shear_bytes);
         const uint8_t* pair[2] = {left, right};
-        stage_images(*h, h->d_in.p, pair, 2, width, height, stride, pitch, s);
-        HIPCK(hipMemsetAsync(h->d_overflow.p, 0, sizeof(int), s));
-        extract_range(*h, h->d_in.p, pitch, 0, 2, s, false, false);
-        stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, s);
-        if (want_pyramid) {
-            h->d_shear.ensure(2 * (size_t)g.shear_bytes);
-            HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, s));
-        }
-        auto d2h = [&](size_t off, const void* src, size_t bytes) {
-            HIPCK(hipMemcpyAsync(hb + off, src, bytes, hipMemcpyDeviceToHost, s));
-        };
-        d2h(h->fo_ovf, h->d_overflow.p, sizeof(int));
-        d2h(h->fo_count, h->d_count.p, 2 * sizeof(int));
-        d2h(h->fo_kps, h->d_kps.p, 2 * cap * sizeof(orbfe_keypoint));
-        d2h(h->fo_desc, h->d_desc.p, 2 * cap * 32);
-        d2h(h->fo_uR, h->d_uR.p, cap * sizeof(float));
-        d2h(h->fo_depth, h->d_depth.p, cap * sizeof(float));
-        d2h(h->fo_status, h->d_status.p, cap);
-        d2h(h->fo_match, h->d_match.p, cap * sizeof(int32_t));
-        if (want_pyramid) d2h(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
+        stage_host(*h, pair, 2, width, height, stride, pitch);
+        // everything after the host copy is one enqueue (a graph replay when graphs are on): both images in,
+        // the 2-image pipeline, stereo, optionally the sheared views, every result out to pinned memory
+        const std::vector<uint64_t> key = {2, bits_of(h->h_in.p), bits_of(h->d_in.p), bits_of(hb),
+                                           bits_of(want_pyramid ? h->d_shear.p : nullptr), (uint64_t)width,
+                                           (uint64_t)height, bits_of(bf), bits_of(fx), (uint64_t)o};
+        run_enqueue(*h, key, s, [&](hipStream_t q) {
+            HIPCK(hipMemcpyAsync(h->d_in.p, h->h_in.p, (size_t)pitch + (size_t)width * height, hipMemcpyHostToDevice, q));
+            HIPCK(hipMemsetAsync(h->d_overflow.p, 0, sizeof(int), q));
+            extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, false);
+            stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q);
+            if (want_pyramid) HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, q));
+            auto d2h = [&](size_t off, const void* src, size_t bytes) {
+                HIPCK(hipMemcpyAsync(hb + off, src, bytes, hipMemcpyDeviceToHost, q));
+            };
+            d2h(h->fo_ovf, h->d_overflow.p, sizeof(int));
+            d2h(h->fo_count, h->d_count.p, 2 * sizeof(int));
+            d2h(h->fo_kps, h->d_kps.p, 2 * cap * sizeof(orbfe_keypoint));
+            d2h(h->fo_desc, h->d_desc.p, 2 * cap * 32);
+            d2h(h->fo_uR, h->d_uR.p, cap * sizeof(float));
+            d2h(h->fo_depth, h->d_depth.p, cap * sizeof(float));
+            d2h(h->fo_status, h->d_status.p, cap);
+            d2h(h->fo_match, h->d_match.p, cap * sizeof(int32_t));
+            if (want_pyramid) d2h(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
+        });
         HIPCK(hipStreamSynchronize(s));
         h->last_in = h->d_in.p;
         h->last_pitch = h->frame_pitch = pitch;
@@ -1549,6 +1620,65 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
             xyr[3 * i + 1] = (int)((kp[i] >> 12) & 0xFFF) - kBorder;
             xyr[3 * i + 2] = (int)(kp[i] >> 24);
         }
+    });
+}
+
+int orbfe_set_graphs(orbfe_handle h, int32_t on) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        h->use_graphs = on != 0;
+        if (!h->use_graphs) h->drop_graphs();
+    });
+}
+
+int orbfe_graph_stats(orbfe_handle h, int64_t* captures, int64_t* launches, int32_t* cached) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (captures) *captures = h->graph_captures;
+        if (launches) *launches = h->graph_launches;
+        if (cached) *cached = (int32_t)h->graphs.size();
+    });
+}
+
+int orbfe_set_octree_kernel(orbfe_handle h, int32_t kernel) {
+    return guarded([&] {
+        if (!h) throw Error(ORBFE_EINVAL, "null handle");
+        if (kernel != 0 && kernel != 1) throw Error(ORBFE_EINVAL, "kernel must be 0 (automatic) or 1 (per-candidate)");
+        h->octree_force = kernel == 1;
+        if (h->W > 0) {  // re-derive the reserved geometry's choice (build_geometry's rule)
+            invalidate_results(*h);
+            h->drop_graphs();
+            Geo& g = h->geo;
+            g.oct_v = h->octree_force || octree_bins_lds_bytes(g, h->maxcell) > 150 * 1024 ? 1 : 0;
+            prepare_kernels(*h);
+        }
+    });
+}
+
+int orbfe_get_octree_kernel(orbfe_handle h, int32_t* kernel, int64_t* bins_lds_bytes) {
+    return guarded([&] {
+        if (!h || !kernel) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->W <= 0) throw Error(ORBFE_ESTATE, "no geometry reserved yet");
+        *kernel = h->geo.oct_v;
+        if (bins_lds_bytes) *bins_lds_bytes = (int64_t)octree_bins_lds_bytes(h->geo, h->maxcell);
+    });
+}
+
+int orbfe_debug_detect_stats(orbfe_handle h, int64_t* stats) {
+    return guarded([&] {
+        if (!h || !stats) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->last_images <= 0 || !h->last_in) throw Error(ORBFE_ESTATE, "run a batch first");
+        const Geo& g = h->geo;
+        DevBuf<int> d;
+        d.ensure(4);
+        HIPCK(hipMemset(d.p, 0, 4 * sizeof(int)));
+        if (g.ncells > 0)
+            HIPCK(launch_detect(g, h->d_cells.p, h->last_in, h->last_pitch, h->d_ws.p, h->d_cell_count.p, h->d_slots.p,
+                                h->last_images, h->last_stream, 0, d.p));
+        HIPCK(hipStreamSynchronize(h->last_stream));
+        int v[4];
+        HIPCK(hipMemcpy(v, d.p, sizeof(v), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 3; ++k) stats[k] = v[k];
     });
 }
 

@@ -63,10 +63,13 @@ hipError_t launch_undistort(const float* xy_in, int n, int stride_in, float* xy_
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s, int variant = 0);
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
-                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant = 0);
+                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant = 0,
+                         int* stats = nullptr);
 size_t octree_lds_bytes(const Geo& g, int maxcell);
 size_t octree_bins_lds_bytes(const Geo& g, int maxcell);
 size_t detect_lds_bytes(const Geo& g);
+// raise the octree kernels' dynamic-LDS attribute for this geometry (outside any stream capture)
+hipError_t prepare_octree(const Geo& g, int maxcell);
 // Geo::oct_v selects k_octree_bins (0) or the per-candidate pass kernel k_octree (1); octab: the
 // per-level Morton tables of k_octree_bins (orbfe_host.hip octree_tables)
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots,

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "orbfe_common.h"
 #include <type_traits>
@@ -61,17 +62,6 @@ __device__ __forceinline__ int wave_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
-}
-
-// Wave issue priority of a kernel (Geo::prio, ORBFE_PRIO): raises a latency-bound stage above the
-// issue-bound waves of the other handles' stages sharing its SIMD (VALU issue goes by priority, then age).
-__device__ __forceinline__ void set_prio(const Geo& g, int k) {
-    switch (g.prio[k]) {
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        case 2: __builtin_amdgcn_s_setprio(2); break;
-        case 3: __builtin_amdgcn_s_setprio(3); break;
-        default: break;
-    }
 }
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -183,11 +173,11 @@ __device__ int block_sum(int v, int* red) {
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 constexpr int kRsSlots = 16;  // staged dwords per thread per pass
 
+#ifdef ORBFE_DEV_VARIANTS  // the round-2 item-mapped kernel, for tools/microbench.py (tools/dbg/build_variant.sh)
 template <int V>  // V: 0 full kernel; ablations for tools/microbench.py: 1 staging only, 2 compute only
 __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                 uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                 const ResizeY* __restrict__ yt) {
-    set_prio(g, kPrioResize);
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     const LevelGeo& L = g.lv[l];
     uint4* s_xa = (uint4*)rs_lds;                        // per group: v_perm selectors, then (a0, a1) weights
@@ -299,6 +289,7 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
         }
     }
 }
+#endif
 
 // k_resize_rows: the same band, with the compute mapped so that a wave's row is uniform.  The block holds
 // R_s row sets of W_g waves (64 W_g >= the level's groups): lane (w % W_g) * 64 + lane of a set owns one
@@ -309,8 +300,7 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 // and 64-bit store address are gone).  Blocks of 256 <= 64 W_g R_s <= 512 threads (the host picks R_s).
 __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                      uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
-                                                     const ResizeY* __restrict__ yt, int wg, int remw) {
-    set_prio(g, kPrioResize);
+                                                     const ResizeY* __restrict__ yt, int wg, int remw, int wgl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     uint32_t* s_src = (uint32_t*)rs_lds;  // staged source rows
     const LevelGeo& L = g.lv[l];
@@ -333,25 +323,33 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     // this thread's group: x selectors / weights straight from the table (issued with the staging loads)
     // remw = 1: the last wave takes the groups past the wg full 64-group chunks (rem < 64 of them) for all
     // rows of the band: lane j owns group wg * 64 + j % rem and rows j / rem, + 64 / rem, ... (a per-lane
-    // row), instead of a mostly idle row-uniform wave per row
-    const int wv = t >> 6, fullw = (nthr >> 6) - remw, nset = fullw / wg;
+    // row), instead of a mostly idle row-uniform wave per row.  A set has wgl <= 8 waves: when a level has
+    // more chunks than that (rows wider than 2 048 px), a set's wave walks chunks c, c + wgl, ...
+    const int wv = t >> 6, fullw = (nthr >> 6) - remw, nset = fullw / wgl;
     const bool remwave = wv >= fullw;
-    const int set = __builtin_amdgcn_readfirstlane(remwave ? 0 : wv / wg);
+    const int set = __builtin_amdgcn_readfirstlane(remwave ? 0 : wv / wgl);
     const int rem = ngrp - wg * 64, lane = t & 63;
     const int rstep = remwave ? 64 / rem : nset;  // rows between a lane's rows in the remainder wave
-    const int grp = remwave ? wg * 64 + lane % rem : (wv - set * wg) * 64 + lane;
     const int row0 = remwave ? lane / rem : set;
-    const bool own = remwave ? lane < rstep * rem : grp < ngrp;
+    int ch = remwave ? wg : wv - set * wgl;       // this wave's first 64-group chunk
+    const int ch_step = remwave ? 1 : wgl, ch_end = remwave ? wg + 1 : wg;
+    int grp = 0;
+    bool own = false;
     uint4 e{}, aa{};
     int sx0 = 0;
-    if (own) {
-        const uint4* xg = (const uint4*)(xt + L.xtab_off);
-        const uint4 q0 = xg[2 * grp], q1 = xg[2 * grp + 1];
-        sx0 = (int)q0.x;
-        auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
-        e = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
-        aa = uint4{q0.y, q0.w, q1.y, q1.w};
-    }
+    auto chunk = [&](int c) {
+        grp = remwave ? wg * 64 + lane % rem : c * 64 + lane;
+        own = remwave ? lane < rstep * rem : grp < ngrp;
+        if (own) {
+            const uint4* xg = (const uint4*)(xt + L.xtab_off);
+            const uint4 q0 = xg[2 * grp], q1 = xg[2 * grp + 1];
+            sx0 = (int)q0.x;
+            auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
+            e = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+            aa = uint4{q0.y, q0.w, q1.y, q1.w};
+        }
+    };
+    chunk(ch);
     // staging by the first 256 threads (blocks have >= 256): compile-time strides, immediate LDS offsets
     if (t < 256) {
         for (int base = 0; base < ndw; base += 256 * kRsSlots) {
@@ -369,49 +367,54 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         }
     }
     __syncthreads();
-    if (!own) return;
     uint8_t* dst = ws + (int64_t)img * g.ws_bytes + L.ws_off + (int64_t)dy0 * L.pitch;
     const __amdgpu_buffer_rsrc_t rd = uniform_rsrc(dst);
-    const int dx = 4 * grp;
-    const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
-    const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-    auto row = [&](int rr) {
-        const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
-        const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
-        const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
-        auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
-            const uint32_t A = lsrc + roff, o = A & 3u;
-            lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-            const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
-            h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
-                                          __builtin_bit_cast(us2, aa.x), 0u, false);
-            h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
-                                          __builtin_bit_cast(us2, aa.y), 0u, false);
-            h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
-                                          __builtin_bit_cast(us2, aa.z), 0u, false);
-            h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
-                                          __builtin_bit_cast(us2, aa.w), 0u, false);
+    for (;;) {
+        if (!own) return;  // only a level's last chunk is partial
+        const int dx = 4 * grp;
+        const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
+        const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
+        auto row = [&](int rr) {
+            const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
+            const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
+            const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
+            auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
+                const uint32_t A = lsrc + roff, o = A & 3u;
+                lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+                h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
+                                              __builtin_bit_cast(us2, aa.x), 0u, false);
+                h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
+                                              __builtin_bit_cast(us2, aa.y), 0u, false);
+                h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
+                                              __builtin_bit_cast(us2, aa.z), 0u, false);
+                h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                              __builtin_bit_cast(us2, aa.w), 0u, false);
+            };
+            uint32_t h0[4], h1[4];
+            taps(r0, h0);
+            taps(r1, h1);
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
+            if (tail) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+            }
+            // pixels past L.w land in the row's pitch padding
+            __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
+                                                  (uint32_t)(rr * L.pitch), 0);
         };
-        uint32_t h0[4], h1[4];
-        taps(r0, h0);
-        taps(r1, h1);
-        uint32_t v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
-        if (tail) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+        if (!remwave) {
+            for (int rr = set; rr < nrow; rr += nset) row(rr);
+        } else {
+            for (int rr = row0; rr < nrow; rr += rstep) row(rr);
         }
-        // pixels past L.w land in the row's pitch padding
-        __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
-                                              (uint32_t)(rr * L.pitch), 0);
-    };
-    if (!remwave) {
-        for (int rr = set; rr < nrow; rr += nset) row(rr);
-    } else {
-        for (int rr = row0; rr < nrow; rr += rstep) row(rr);
+        ch += ch_step;
+        if (ch >= ch_end) return;
+        chunk(ch);
     }
 }
 
@@ -507,7 +510,9 @@ __device__ __forceinline__ uint32_t fast_m_pair(const uint32_t* R) {
 
 __device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
 
-constexpr int kFdCells = 4;  // cells per k_detect wavefront (the next cell's ROI loads overlap this one)
+// cells per k_detect wavefront: 4 (the next cell's ROI loads overlap this one), or 1 for batches too small to
+// give the chip >= 8 waves per CU that way (a frame pair: 610 waves of 4 cells, 2 440 of one)
+constexpr int kFdCells = 4;
 
 __device__ __forceinline__ int lanes_below(uint64_t b) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
@@ -525,11 +530,11 @@ __host__ __device__ inline int detect_roi_elems(const Geo& g, int rp) {
 // 5 waves per SIMD (<= 96 VGPRs; 4 for the wider / taller ROI variants, which need the registers) and
 // <= 8 KiB of LDS for KITTI / EuRoC cells: detect is bound by how many
 // cells are in flight per CU (16 -> 10 resident waves costs +32 %, tools/microbench.py variant 8).
-template <int V, int RP, int NS>
+template <int V, int RP, int NS, int CPW>
 __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
-                                               int* __restrict__ cell_count, uint32_t* __restrict__ slots) {
-    set_prio(g, kPrioDetect);
+                                               int* __restrict__ cell_count, uint32_t* __restrict__ slots,
+                                               int* __restrict__ stats) {
     constexpr int S = RP / 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // ROI (max_rh rows x RP u16); after the M stage the same bytes stage the minTh survivors (u32 records)
@@ -546,7 +551,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
     int bx, img;
     xcd_block(bx, img);  // neighbouring cells' ROIs overlap by 6 rows / columns: keep them in one L2
     const int lane = threadIdx.x;
-    const int c_first = bx * kFdCells, c_last = min(c_first + kFdCells, g.ncells);
+    const int c_first = bx * CPW, c_last = min(c_first + CPW, g.ncells);
     // ROI staging, 8 lanes per row (dwords 2d, 2d + 1), 8 rows per step (NS / 2 steps): lane d loads two
     // dwords of the row from the 4-byte aligned start of column -1 and takes dword 2d + 2 from its
     // neighbour lane (DPP row_shl:1) to re-align 8 bytes with v_alignbyte (rows are <= 59 px, so 16
@@ -806,6 +811,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             }
         };
         const bool collide = npq + npa > cap;
+        // orbfe_debug_detect_stats: cells that took the one-pass path despite two thresholds (the queues met)
+        if (stats && lane == 0 && two && collide) atomicAdd(&stats[1], 1);
         int total = 0;
         if (two && !collide) {
             int t0, t1;
@@ -817,6 +824,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             nms_stage(pq + cap - 1, -1, nna, max(g.ini_th, 1), 0, t0, t1);
             total = t0;
             if (t0 == 0) {  // minTh fallback: every pair of B (the A pairs' M is recomputed, identically)
+                if (stats && lane == 0) atomicAdd(&stats[2], 1);
                 const int nnb = m_stage(pq, 1, npq, max(g.min_th, 1));
                 nms_stage(pq, 1, nnb, max(g.min_th, 1), 0, t0, t1);
                 total = t0;
@@ -841,6 +849,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             }
         }
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
+        if (stats && lane == 0) atomicAdd(&stats[0], 1);
         };
         process();
         __syncthreads();  // the next cell overwrites the ROI and the M map
@@ -935,7 +944,6 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                                                 uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
                                                 int* __restrict__ overflow, int maxcell, int stop,
                                                 long long* __restrict__ prof) {
-    set_prio(g, kPrioOctree);
     // stop (tools/microbench.py ablations): 1 after the candidate gather, 2 after the initial columns,
     // 3 after the full-division phase, 16 + l only level l, 64 + 8 l + n only level l and stop before
     // pass n; 0 = the whole algorithm
@@ -1436,8 +1444,9 @@ __device__ __forceinline__ void bin_add_runs(uint32_t* hist, uint32_t* bmax, uin
     if (pb == b) m = max(m, pv);
     pb = dpp_shr<8>(nob, b); pv = dpp_shr<8>(0u, m);
     if (pb == b) m = max(m, pv);
-    const uint32_t nextb = (uint32_t)__shfl_down((int)b, 1, 64);
-    const bool tail = valid && ((lane & 15) == 15 || nextb != b);
+    // run tails from the ballot, like the heads: the next lane starts a run, holds no key or has left the
+    // caller's key loop (a shuffle from an inactive lane would read 0, i.e. bin 0: ADVICE r3)
+    const bool tail = valid && ((lane & 15) == 15 || lane == 63 || ((heads >> (lane + 1)) & 1ull));
     if (tail) atomicMax(&bmax[b], m);
 }
 
@@ -1494,7 +1503,6 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
                                                             uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
                                                             int* __restrict__ overflow, int maxcell,
                                                             long long* __restrict__ prof) {
-    set_prio(g, kPrioOctree);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int s_K, s_S, s_cur, s_nd;
     const int img = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
@@ -2087,7 +2095,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                                                     const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                     const uint32_t* __restrict__ tab) {
-    set_prio(g, kPrioOrb);
     __shared__ float4 s_pat[256];
     __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: (byte mask, m10 byte weights)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
@@ -2252,28 +2259,19 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         // ---- stage keypoint j: the previous keypoint's reads of src / hb are complete (waited before its
         //      ballots, which precede this point)
         wave_sync_lds();
-#if !defined(ORBFE_X_NOSTAGE)  // experiment: no window staging (garbage window), wrong bits
         if (inside(cx)) commit();
         else stage_border(cx, cy);
-#endif
         wave_sync_lds();
         const int ccx = cx, ccy = cy;
         if (j + 1 < nk) {  // next keypoint's loads in flight during this one's compute
             const uint32_t k = key_of(j + 1);
             cx = (int)(k & 0xFFF);
             cy = (int)((k >> 12) & 0xFFF);
-#if !defined(ORBFE_X_NOSTAGE)
             if (inside(cx)) issue(cx, cy);
-#endif
         }
         // ---- horizontal taps of the disc's (row pair, group) items
-#if defined(ORBFE_X_NOH)  // experiment (tools/dbg/build_variant.sh): no horizontal pass, wrong bits
-        constexpr int kHRun = 0;
-#else
-        constexpr int kHRun = kOrbHItems;
-#endif
 #pragma unroll
-        for (int k = 0; k < kHRun; ++k) {
+        for (int k = 0; k < kOrbHItems; ++k) {
             {  // lanes without an item run the dummy one (orb_tables)
                 typedef __attribute__((address_space(3))) uint32_t lds_w32;
                 const lds_w32* q = (const lds_w32*)(uintptr_t)(hit[k] & 0xFFFFu);
@@ -2303,9 +2301,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                     u32x4{pk(h[0][0], h[1][0]), pk(h[0][1], h[1][1]), pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
             }
         }
-#if defined(ORBFE_X_NOCENT)  // experiment: no centroid / angle, wrong angles and bits
-        const float angle = 0.f, a = 1.f, b = 0.f;
-#else
         // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15)
         uint32_t a10 = 0, a01 = 0, a1 = 0;
 #pragma unroll
@@ -2321,7 +2316,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         const float angle = fast_atan2_uniform(m01, m10);
         float b, a;
         glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
-#endif
         wave_sync_lds();  // hb complete
         // ---- steered BRIEF with the vertical taps per sample: sample (row, col) is blurred row o = row + 18
         //      (H rows o .. o + 6), column c = col + 21.  rint by the 1.5 * 2^23 trick: the f32 bits are
@@ -2335,13 +2329,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         typedef __attribute__((address_space(3))) const uint32_t lds_u32;
         const uint32_t kc = (uint32_t)(uintptr_t)(lds_u32*)hb + (uint32_t)(4 * (9 * kHDw + 21)) -
                             (uint32_t)(4 * kHDw) * 0xA00000u - (__float_as_uint(12582912.0f) << 2);
-#if defined(ORBFE_X_NOBRIEF)  // experiment: no BRIEF samples, wrong bits
-        constexpr int kBRun = 0;
-#else
-        constexpr int kBRun = 4;
-#endif
 #pragma unroll 1
-        for (int i = 0; i < kBRun; ++i) {
+        for (int i = 0; i < 4; ++i) {
             const float4 pt = s_pat[lane + 64 * i];
             uint32_t v2[2];
 #pragma unroll
@@ -2354,15 +2343,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 static_assert(4 * kHDw == 0xA0, "H row-pair stride of the v_mad_u32_u24 operand");
                 uint32_t addr;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(addr) : "v"(xb >> 1), "s"(0xA0u), "v"((yb << 2) + kc));
-#if defined(ORBFE_X_NOCONF)  // experiment (tools/dbg/build_variant.sh): conflict-free reads, wrong bits
-                lds_u32* p = (lds_u32*)(uintptr_t)((uint32_t)(uintptr_t)(lds_u32*)hb + 4 * (lane & 31) + (addr & 0x40));
-                const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
-#elif defined(ORBFE_X_NOBRIEFLDS)  // experiment: no BRIEF LDS reads at all, wrong bits
-                const uint32_t p0 = addr, p1 = addr ^ xb, p2 = addr + yb, p3 = xb ^ yb;
-#else
                 lds_u32* p = (lds_u32*)(uintptr_t)addr;
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
-#endif
                 const uint32_t sh = xb << 4;
                 uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p1, p0, sh)), w2(18, 34), 32768u, false);
                 s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p2, p1, sh)), w2(48, 56), s, false);
@@ -2476,7 +2458,6 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
 // Also writes the compact (x, octave) record of every right keypoint.
 __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
-    set_prio(g, kPrioBucket);
     extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
     __shared__ int scan_tmp[257];
     const int pr = blockIdx.x, t = threadIdx.x;
@@ -2568,7 +2549,6 @@ __device__ __forceinline__ void sheared_words(__amdgpu_buffer_rsrc_t rs, uint32_
 }
 
 __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
-    set_prio(g, kPrioStereo);
     __shared__ int sad[16][11];
     // the 11 x 11 left and 11 x 21 right windows as u16 pixel + 512: left columns (2k, 2k + 1) per dword,
     // right columns (2k, 2k + 1) and (2k + 1, 2k + 2) per dword (both alignments of a shift's window)
@@ -2861,23 +2841,28 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
     // k_resize, 1 / 2 = its staging-only / compute-only ablations
     if (variant == 0 || variant == 3 || variant == 5) {
         // a level whose groups leave a last chunk of fewer than 40 (of 64) takes it in one remainder wave
-        // (variant 5 / ORBFE_RS_REM=0: never, every chunk row-uniform)
-        static const int rs_rem = [] {
-            const char* e = std::getenv("ORBFE_RS_REM");
-            return e ? std::atoi(e) : 1;
-        }();
+        // (variant 5: never, every chunk row-uniform); at most 8 waves per row set, each walking several
+        // chunks on rows wider than 2 048 px, so the block stays within __launch_bounds__(512)
         const int ngrp = (L.w + 3) / 4, rem = ngrp % 64;
-        const int remw = (variant != 5 && rs_rem != 0 && ngrp >= 64 && rem > 0 && rem < 40) ? 1 : 0;
-        const int wg = remw ? ngrp / 64 : (ngrp + 63) / 64;
-        const int sets = std::max(1, (4 - remw + wg - 1) / wg);  // >= 256 threads per block (the staging threads)
-        hipLaunchKernelGGL(k_resize_rows, grid, dim3(64 * (wg * sets + remw)), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g,
-                           l, in, in_pitch, ws, xt, yt, wg, remw);
+        const int wg0 = (ngrp + 63) / 64;
+        const int remw = (variant != 5 && ngrp >= 64 && wg0 <= 8 && rem > 0 && rem < 40) ? 1 : 0;
+        const int wg = remw ? ngrp / 64 : wg0;
+        const int wgl = std::min(wg, 8 - remw);
+        const int sets = std::max(1, (4 - remw + wgl - 1) / wgl);  // >= 256 threads per block (the staging threads)
+        const int threads = 64 * (wgl * sets + remw);
+        if (threads < 256 || threads > 512) return hipErrorInvalidConfiguration;
+        hipLaunchKernelGGL(k_resize_rows, grid, dim3(threads), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in, in_pitch,
+                           ws, xt, yt, wg, remw, wgl);
         return hipGetLastError();
     }
+#ifdef ORBFE_DEV_VARIANTS
     const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
     auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;  // variant 4: k_resize<0>
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();
+#else
+    return hipErrorInvalidValue;  // the microbench variants exist only in ORBFE_DEV_VARIANTS builds
+#endif
 }
 
 int detect_rp(const Geo& g) { return g.max_rw + 3 <= 48 ? 48 : g.max_rw + 3 <= 64 ? 64 : 96; }
@@ -2887,32 +2872,45 @@ size_t detect_lds_bytes(const Geo& g) {
     return 2 * (size_t)detect_roi_elems(g, detect_rp(g)) + (size_t)detect_rp(g) * (g.max_wh + 2) + 2 * (size_t)g.fd_pq;
 }
 
+// cells per wave for a batch: 4 unless that leaves fewer than 8 waves per CU (variant 4 / 1 force 4 / 1)
+int detect_cpw(const Geo& g, int n_images, int variant) {
+    if (variant == 4) return 4;
+    if (variant == 5) return 1;
+    return (int64_t)n_images * ((g.ncells + kFdCells - 1) / kFdCells) < 8 * 256 ? 1 : kFdCells;
+}
+
 template <int RP, int NS>
 static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
-                             int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
+                             int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant, int* stats) {
+    const int cpw = detect_cpw(g, n_images, variant);
+    const dim3 grid((g.ncells + cpw - 1) / cpw, n_images), blk(64);
+#ifdef ORBFE_DEV_VARIANTS
     // variants 8 / 9: the full kernel with 6 / 12 KiB of extra (unused) LDS, to measure how detect
-    // time depends on occupancy (tools/microbench.py)
+    // time depends on occupancy; 1 / 2 / 3: the ablations (tools/microbench.py)
     const size_t lds = detect_lds_bytes(g) + (variant == 8 ? 6144 : variant == 9 ? 12288 : 0);
-    const dim3 grid((g.ncells + kFdCells - 1) / kFdCells, n_images), blk(64);
-    auto k = variant == 1 ? k_detect<1, RP, NS> : variant == 2 ? k_detect<2, RP, NS> : variant == 3 ? k_detect<3, RP, NS>
-                                                                                           : k_detect<0, RP, NS>;
-    hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots);
+    auto k = variant == 1 ? k_detect<1, RP, NS, kFdCells> : variant == 2 ? k_detect<2, RP, NS, kFdCells>
+           : variant == 3 ? k_detect<3, RP, NS, kFdCells> : cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>;
+#else
+    const size_t lds = detect_lds_bytes(g);
+    auto k = cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>;
+#endif
+    hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots, stats);
 }
 
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
-                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant) {
+                         int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant, int* stats) {
     // ROIs of at most 48 rows (KITTI, EuRoC) stage from 12 registers, taller ones (<= 64) from 16
     const bool tall = g.max_rh > 48;
     switch (detect_rp(g)) {
         case 48:
-            if (tall) launch_detect_rp<48, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
-            else launch_detect_rp<48, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            if (tall) launch_detect_rp<48, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant, stats);
+            else launch_detect_rp<48, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant, stats);
             break;
         case 64:
-            if (tall) launch_detect_rp<64, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
-            else launch_detect_rp<64, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+            if (tall) launch_detect_rp<64, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant, stats);
+            else launch_detect_rp<64, 12>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant, stats);
             break;
-        default: launch_detect_rp<96, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant);
+        default: launch_detect_rp<96, 16>(g, cells, in, in_pitch, ws, cell_count, slots, n_images, s, variant, stats);
     }
     return hipGetLastError();
 }
@@ -2929,55 +2927,87 @@ size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
     return ob_carve(g.max_ncap, g.oct_bins_max, maxcell, g.oct_tab_max, g.oct_kblk_max, [](int, size_t) {});
 }
 
+// gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB on request.  Raised (never lowered) once per
+// process and kernel, when a geometry is built (orbfe_host.hip prepare_kernels): launches, which may be
+// inside a graph capture, only check.
+static int g_lds_attr[2] = {64 * 1024, 64 * 1024};  // k_octree_bins, k_octree
+static std::mutex g_lds_mu;
+
+hipError_t prepare_octree(const Geo& g, int maxcell) {
+    const size_t need[2] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell)};
+    const void* fn[2] = {(const void*)k_octree_bins, (const void*)k_octree};
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    for (int k = 0; k < 2; ++k) {
+        if ((int)need[k] <= g_lds_attr[k] || need[k] > 160 * 1024) continue;
+        const hipError_t e = hipFuncSetAttribute(fn[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[k]);
+        if (e != hipSuccess) return e;
+        g_lds_attr[k] = (int)need[k];
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots,
                          const uint32_t* octab, uint32_t* kd, uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow,
                          int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
     if (g.oct_v == 0) {
         const size_t lds = octree_bins_lds_bytes(g, maxcell);
-        if (lds > 64 * 1024) {
-            const hipError_t e =
-                hipFuncSetAttribute((const void*)k_octree_bins, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
+        if ((int)lds > g_lds_attr[0]) return hipErrorInvalidConfiguration;  // prepare_octree was not run
         hipLaunchKernelGGL(k_octree_bins, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells, cell_count, slots,
                            octab, lvl_kp, lvl_count, overflow, maxcell, prof);
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
-    if (lds > 64 * 1024) {  // gfx950: up to 160 KiB per workgroup, above 64 KiB on request
-        const hipError_t e = hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
+    if ((int)lds > g_lds_attr[1]) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL(k_octree, dim3(n_images, g.nlevels), dim3(kOctThreads), lds, s, g, cells, cell_count, slots, kd, kn,
                        lvl_kp, lvl_count, overflow, maxcell, variant, prof);
     return hipGetLastError();
+}
+
+static int orb_waves(const Geo& g, int kpw) {
+    int waves = 0;
+    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + kpw - 1) / kpw;
+    return waves;
 }
 
 template <int NW, int KPW>
 static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
                           const uint32_t* tab, hipStream_t s) {
-    int waves = 0;  // most waves an image can need: KPW keypoints per wave, per level
-    for (int l = 0; l < g.nlevels; ++l) waves += (g.lv[l].kp_cap + KPW - 1) / KPW;
+    const int waves = orb_waves(g, KPW);  // most waves an image can need: KPW keypoints per wave, per level
     hipLaunchKernelGGL((k_orb<NW, KPW>), dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws,
                        lvl_kp, lvl_count, out_kp, out_desc, out_count, tab);
 }
 
-// variant (microbench): 0 = production (4 waves per workgroup, 8 keypoints per wave: 953 -> 914 us per 256
-// pairs against 4, same-box A/B); 8: 8 waves; 2 / 9 / 10: 2 / 4 / 16 keypoints per wave
+// keypoints per wave for a batch: 8 (4 waves per workgroup: 953 -> 914 us per 256 pairs against 4, same-box
+// A/B, round 1) while the batch gives >= 16 waves per CU that way, else 4, else 2 (a frame pair: 508 waves of
+// 8 keypoints, 2 028 of 2).  Variants (microbench): 1 / 9 / 2 force 8 / 4 / 2.
+int orb_kpw(const Geo& g, int n_images, int variant) {
+    if (variant == 1) return 8;
+    if (variant == 9) return 4;
+    if (variant == 2 || variant == 12) return 2;
+    for (int k : {8, 4})
+        if ((int64_t)orb_waves(g, k) * n_images >= 16 * 256) return k;
+    return 2;
+}
+
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
                       const uint32_t* tab, hipStream_t s, int variant) {
-    if (variant == 8)
+#ifdef ORBFE_DEV_VARIANTS
+    if (variant == 8) {
         launch_orb_nw<8, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
-    else if (variant == 2)
-        launch_orb_nw<4, 2>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
-    else if (variant == 10)
+        return hipGetLastError();
+    }
+    if (variant == 10) {
         launch_orb_nw<4, 16>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
-    else if (variant == 9)
-        launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
-    else
-        launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        return hipGetLastError();
+    }
+#endif
+    switch (orb_kpw(g, n_images, variant)) {
+        case 2: launch_orb_nw<4, 2>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s); break;
+        case 4: launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s); break;
+        default: launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+    }
     return hipGetLastError();
 }
 

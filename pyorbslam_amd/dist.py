@@ -72,19 +72,42 @@ def unpack(kp_cap: int, rec: np.ndarray) -> dict:
     return out
 
 
-def gather_records(records, dst: int = 0):
+_GATHER_BUF: dict = {}
+
+
+def gather_buffer(world: int, records):
+    """dst's receive buffer for gather_records: one (world * local_pairs, record_bytes) tensor per (shape,
+    dtype, device), allocated on first use and reused by every later gather of that shape."""
+    import torch
+    key = (world, tuple(records.shape), records.dtype, str(records.device))
+    buf = _GATHER_BUF.get(key)
+    if buf is None:
+        buf = torch.empty((world * records.shape[0],) + tuple(records.shape[1:]), dtype=records.dtype,
+                          device=records.device)
+        _GATHER_BUF[key] = buf
+    return buf
+
+
+def gather_records(records, dst: int = 0, out=None):
     """records: (local_pairs, record_bytes) uint8 torch tensor of this rank — on the GPU with backend "nccl"
     (RCCL over xGMI), on the CPU with gloo.  Every rank must pass the same shape (the batched-frames mode
-    gives every rank the same pair count; pad otherwise).  One collective, a gather to `dst`: returns the
-    (world * local_pairs, record_bytes) tensor on dst, rank-major = global pair order, None elsewhere."""
-    import torch
+    gives every rank the same pair count; pad otherwise).  One collective, a gather to `dst` straight into
+    rank-major slices of one preallocated buffer (`out`, or gather_buffer's; no per-rank tensors, no
+    concatenation): returns that (world * local_pairs, record_bytes) tensor on dst — global pair order —,
+    None elsewhere.  The returned buffer is reused by the next gather of the same shape."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
     if world == 1:
         return records
-    outs = [torch.empty_like(records) for _ in range(world)] if rank == dst else None
-    dist.gather(records, gather_list=outs, dst=dst)
-    return torch.cat(outs, 0) if rank == dst else None
+    if rank == dst:
+        full = gather_buffer(world, records) if out is None else out
+        if tuple(full.shape) != (world * records.shape[0],) + tuple(records.shape[1:]):
+            raise ValueError("gather output buffer has the wrong shape")
+        parts = list(full.view((world,) + tuple(records.shape)).unbind(0))  # contiguous rank slices
+    else:
+        full, parts = None, None
+    dist.gather(records, gather_list=parts, dst=dst)
+    return full
 
 
 def gather_results(records: np.ndarray, n_pairs_total: int, device=None, dst: int = 0):

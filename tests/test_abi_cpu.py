@@ -12,7 +12,7 @@ HEADER = ROOT / "include" / "orbfe.h"
 def declared():
     txt = HEADER.read_text()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(orbfe_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(orbfe_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_header_declares_entry_points():

@@ -52,3 +52,16 @@ def test_m0_only_for_writelane(tmp_path):
                 ins = line.split("//")[0].split()
                 op = next((t for t in ins if re.match(r"^[sv]_|^ds_|^buffer_|^global_", t)), "")
                 assert op in ("s_mov_b32", "v_writelane_b32"), f"{n}: unexpected M0 use: {line.strip()}"
+
+
+def test_product_library_reads_no_environment():
+    """no environment variable can change a kernel path of the production library —
+    it imports no getenv and names no ORBFE_* variable (the development knobs of earlier rounds live only in
+    tools/dbg/build_variant.sh builds, ORBFE_DEV_VARIANTS)."""
+    if not LIB.exists():
+        pytest.skip("liborbfe.so missing")
+    und = subprocess.run(["nm", "-D", "--undefined-only", str(LIB)], check=True, capture_output=True, text=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", und), "liborbfe.so imports getenv"
+    strs = subprocess.run(["strings", str(LIB)], check=True, capture_output=True, text=True).stdout
+    names = set(re.findall(r"\bORBFE_[A-Z0-9_]+\b", strs)) - {"ORBFE_NSTAGES"}
+    assert not names, f"liborbfe.so names environment-style knobs: {sorted(names)}"

@@ -2,7 +2,14 @@
 (SQ_INSTS_VALU = wave-instructions, summed over the chip).  Every stage of this pipeline is bound by
 VALU issue (integer / packed-f16 stencils, compaction): bench.py prices each stage's measured time
 against the chip's issue rate with these counts (profiles/valu.json, like traffic.json for bytes).
-usage: python tools/valu.py PMC_DIR WORKLOAD OUT_JSON"""
+usage: python tools/valu.py PMC_DIR WORKLOAD OUT_JSON [BUSY_PMC_DIR]
+
+BUSY_PMC_DIR (optional): a pass with SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE over the
+same command.  Per stage it adds the VALU-busy fraction from busy cycles rather than from a class peak:
+  valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)   (SQ_* count quad-cycles summed
+  over waves; GRBM_GUI_ACTIVE is summed over the 8 XCDs, MI355X_MICROARCH.md), the issue-stall share
+  SQ_WAIT_INST_ANY / SQ_BUSY_CYCLES, and the effective clock GRBM_GUI_ACTIVE / 8 / the stage's dispatch time
+  is left to the reader (bench.py has the times).  Stored as <workload>["busy"][stage]."""
 import collections
 import csv
 import glob
@@ -39,6 +46,25 @@ def main():
     except Exception:
         pass
     data[workload] = {st: v["valu_inst"] for st, v in res.items()}
+    if len(sys.argv) > 4:
+        bd = sys.argv[4]
+        act, busy, wait, gui = (per_kernel(bd, c) for c in ("SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES",
+                                                             "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"))
+        busy_out = {}
+        for st, ks in STAGES.items():
+            a = sum(sum(act.get(k, [])) for k in ks)
+            g = sum(sum(gui.get(k, [])) for k in ks)
+            b = sum(sum(busy.get(k, [])) for k in ks)
+            w = sum(sum(wait.get(k, [])) for k in ks)
+            if g <= 0:
+                continue
+            busy_out[st] = {"valu_busy": round(4 * a / (1024 * g / 8), 4),
+                            "wait_inst_any_over_busy": round(w / b, 4) if b else None,
+                            "SQ_ACTIVE_INST_VALU": a, "SQ_BUSY_CYCLES": b, "SQ_WAIT_INST_ANY": w, "GRBM_GUI_ACTIVE": g,
+                            "dispatches": len(gui.get(ks[0], []))}
+            print(f"{st:9s} VALU-busy {busy_out[st]['valu_busy']:.3f}  wait_inst/busy "
+                  f"{busy_out[st]['wait_inst_any_over_busy']}")
+        data[workload]["busy"] = busy_out
     data[workload + "_detail"] = res
     data[workload + "_meta"] = stamp()
     json.dump(data, open(out, "w"), indent=1, sort_keys=True)
