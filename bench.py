@@ -406,12 +406,15 @@ def max_over_ranks(v, dev, world):
     return float(t.item())
 
 
-def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
+def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True) -> dict:
     """The shard's pairs streamed from pinned host memory every step, per handle: its images H2D on a copy
     stream into one of two device buffers (the handle starts as soon as ITS chunk has landed, while the
-    next chunks are still on the link), its batch, its pairs' records packed (k_pack) and brought back D2H
-    into pinned memory on a second copy stream.  Timed like a step (barrier + synchronize, max over ranks);
-    the records of the last step are checked against the handles' own results."""
+    next chunks are still on the link), its batch, and its pairs' records back in pinned host memory —
+    zero_copy (default): k_pack writes them straight into the pinned buffer over PCIe (device-visible
+    hipHostMalloc memory, no device staging buffer and no copy-engine transfer competing with the H2D
+    copies); otherwise packed into device memory and copied D2H on a second copy stream.  Timed like a step
+    (barrier + synchronize, max over ranks); the records of the last step are checked against the handles'
+    own results."""
     import torch
     from pyorbslam_amd import dist as D
     from pyorbslam_amd._lib import call
@@ -420,7 +423,7 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
     hin = torch.from_numpy(host).pin_memory()
     dbuf = [torch.empty(hin.shape, dtype=torch.uint8, device=dev) for _ in range(2)]
     rb = D.record_bytes(sh.fes[0].kp_cap)
-    drec = [torch.empty((n, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
+    drec = [] if zero_copy else [torch.empty((n, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
     hrec = [torch.empty((n, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
     h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     ev = {name: [[torch.cuda.Event() for _ in range(H)] for _ in range(2)] for name in ("in", "free", "out")}
@@ -439,16 +442,17 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
                 dbuf[b][2 * o0:2 * o1].copy_(hin[2 * o0:2 * o1], non_blocking=True)
                 ev["in"][b][j].record(h2d)
             st.wait_event(ev["in"][b][j])
-            if seen[b]:
+            if seen[b] and not zero_copy:
                 st.wait_event(ev["out"][b][j])         # drec[b] rows of handle j have left the device
             f.enqueue(dbuf[b][2 * o0:2 * o1], c, sh.bf, sh.fx, stream_ptr=st.cuda_stream)
-            call("orbfe_batch_pack_device", f.handle, C.c_void_p(drec[b][o0].data_ptr()), rb, 0, c,
-                 C.c_void_p(st.cuda_stream))
+            dst = hrec[b][o0] if zero_copy else drec[b][o0]
+            call("orbfe_batch_pack_device", f.handle, C.c_void_p(dst.data_ptr()), rb, 0, c, C.c_void_p(st.cuda_stream))
             ev["free"][b][j].record(st)
-            with torch.cuda.stream(d2h):
-                d2h.wait_event(ev["free"][b][j])
-                hrec[b][o0:o1].copy_(drec[b][o0:o1], non_blocking=True)
-                ev["out"][b][j].record(d2h)
+            if not zero_copy:
+                with torch.cuda.stream(d2h):
+                    d2h.wait_event(ev["free"][b][j])
+                    hrec[b][o0:o1].copy_(drec[b][o0:o1], non_blocking=True)
+                    ev["out"][b][j].record(d2h)
         seen[b] = True
 
     el = timed(step, steps, warmup, dev, world)
@@ -467,11 +471,14 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup) -> dict:
             "h2d_bytes_per_pair": int(in_b // n), "d2h_bytes_per_pair": int(rb),
             "h2d_GBs_per_gpu": round(in_b * steps / el / 1e9, 2), "d2h_GBs_per_gpu": round(out_b * steps / el / 1e9, 2),
             "pcie_bound_pairs_per_s_per_gpu": round(PCIE_PEAK_GBS * 1e9 / (in_b / n), 1),
-            "record_check": ok,
+            "record_check": ok, "records": "k_pack into pinned host memory" if zero_copy else "k_pack + D2H copy",
             "what": "per handle: its images H2D from pinned host memory (copy stream, two device buffers), its batch, "
-                    "its pairs' packed records D2H into pinned memory (second copy stream); chunks of later handles "
-                    "stream while earlier handles compute; PCIe Gen5 x16 spec 63 GB/s per direction bounds the H2D "
-                    "leg (tools/dbg/pcie_probe.py measured 57 GB/s H2D alone, 45 GB/s with the D2H leg running)"}
+                    "its pairs' records packed " + ("by k_pack straight into pinned host memory (zero-copy stores over "
+                                                    "PCIe)" if zero_copy else "on the device and copied D2H (second "
+                                                                               "copy stream)")
+                    + "; chunks of later handles stream while earlier handles compute; PCIe Gen5 x16 spec 63 GB/s per "
+                      "direction bounds the H2D leg (tools/dbg/pcie_probe.py measured 57 GB/s H2D alone, 45 GB/s with "
+                      "a D2H copy running)"}
 
 
 # ----------------------------------------------------------------------------------- evidence lookups
@@ -650,6 +657,8 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="skip the timed rank-0 gather (N > 1)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (64 pairs in total) line")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed (PCIe-inclusive) line")
+    ap.add_argument("--host-fed-copy", action="store_true",
+                    help="host-fed records via a device buffer + D2H copy instead of k_pack into pinned host memory")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 tracking-loop latency (N = 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 EuRoC line (N = 1, KITTI runs only)")
     args = ap.parse_args()
@@ -746,7 +755,7 @@ def main():
     # ---- host-fed (PCIe-inclusive) rate of the same workload
     hf = None
     if extras and not args.no_host_fed:
-        hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2)
+        hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2, zero_copy=not args.host_fed_copy)
 
     # ---- C4's rank share (8 pairs) on this GPU, and C5 (EuRoC), N = 1
     share = None

@@ -215,7 +215,9 @@ int orbfe_batch_status(orbfe_handle h, int32_t* overflow);
  * (kp_cap x orbfe_keypoint each) | descriptors L, R (kp_cap x 32 B each) | u_right, depth (kp_cap x f32)
  * | status (kp_cap x i8), padded to 16 bytes: orbfe_batch_record_bytes.  orbfe_batch_pack_device writes
  * pairs [pair0, pair0 + n_pairs) of the last stereo batch to d_records (n_pairs x rec_bytes, 4-byte
- * aligned) on hip_stream, without synchronising. */
+ * aligned) on hip_stream, without synchronising.  d_records is device memory or page-locked host memory
+ * (hipHostMalloc): the records then go over PCIe straight into host memory (no device staging buffer, no
+ * copy-engine transfer); pageable memory is refused with ORBFE_EINVAL. */
 int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes);
 int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0, int32_t n_pairs,
                             void* hip_stream);

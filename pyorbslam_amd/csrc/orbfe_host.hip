@@ -1235,6 +1235,19 @@ int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_byte
             throw Error(ORBFE_EINVAL, "pair range outside the last stereo batch");
         if (rec_bytes != record_bytes(h->geo.kp_cap)) throw Error(ORBFE_EINVAL, "record size does not match kp_cap");
         if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
+        // device memory, or page-locked host memory the device can address (k_pack then writes the records over
+        // PCIe straight into host memory); pageable host memory is refused instead of faulting on the device
+        hipPointerAttribute_t pa{};
+        if (hipPointerGetAttributes(&pa, d_records) != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error(ORBFE_EINVAL, "records buffer is neither device memory nor registered host memory");
+        }
+        if (pa.type == hipMemoryTypeHost) {
+            if (!pa.devicePointer) throw Error(ORBFE_EINVAL, "host records buffer is not mapped for the device");
+            d_records = (uint8_t*)pa.devicePointer;
+        } else if (pa.type != hipMemoryTypeDevice && pa.type != hipMemoryTypeManaged) {
+            throw Error(ORBFE_EINVAL, "records buffer is neither device memory nor registered host memory");
+        }
         PackArgs a{h->d_count.p, h->d_kps.p, h->d_desc.p, h->d_uR.p, h->d_depth.p, h->d_status.p, h->geo.kp_cap,
                    rec_bytes};
         // the records are read after the batch that produced them, on whichever stream the caller packs

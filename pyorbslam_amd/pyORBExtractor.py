@@ -209,20 +209,44 @@ class ORBextractor:
 
 
 def as_gray_u8(image) -> np.ndarray:
-    """The reference caster's input rules (opencv_type_casters.h:184-200): 2-D uint8, or 3-D with one
-    channel; int32 / float32 are undefined behaviour downstream and every other dtype raises."""
+    """The reference caster's input rules (opencv_type_casters.h:163-200): 2-D uint8, or 3-D with one channel;
+    int32 / float32 are undefined behaviour downstream and every other dtype raises.
+
+    Strides: the caster builds cv::Mat(nh, nw, CV_8UC1, info.ptr) from the buffer's first element and IGNORES
+    numpy's strides (opencv_type_casters.h:200), so a non-contiguous view (a sliced ROI, every other row, ...)
+    is read as nh x nw consecutive bytes starting at its first element.  The same bytes are read here (a
+    zero-copy (nh, nw) view over them), so such a view yields the reference's keypoints, not those of the
+    pixels the view shows.  Where those bytes would run past the end of the array's buffer (e.g. a
+    negative-stride view), the reference reads out of bounds; this raises RuntimeError instead."""
     img = np.asarray(image)
     if img.ndim not in (2, 3):
         raise RuntimeError(f"Unsupported dim {img.ndim}, only support 2d, or 3-d")
     if img.dtype != np.uint8:
         # the reference casts int32/float32 to CV_32S/CV_32F (undefined downstream) and rejects the rest
         raise RuntimeError("Unsupported type, only support uchar, int32, float")
+    if img.ndim == 3 and img.shape[2] != 1:
+        raise RuntimeError("multi-channel images are undefined behaviour in the reference (CV_8UC1 assert "
+                           "compiled out); pass a grayscale image")
+    nh, nw = int(img.shape[0]), int(img.shape[1])
     if img.ndim == 3:
-        if img.shape[2] != 1:
-            raise RuntimeError("multi-channel images are undefined behaviour in the reference (CV_8UC1 assert "
-                               "compiled out); pass a grayscale image")
         img = img[:, :, 0]
-    return np.ascontiguousarray(img)
+    if img.flags.c_contiguous or nh * nw == 0:
+        return np.ascontiguousarray(img)
+    return _stride_ignoring_view(img, nh, nw)
+
+
+def _stride_ignoring_view(img: np.ndarray, nh: int, nw: int) -> np.ndarray:
+    """nh x nw consecutive bytes from img's first element, as a (nh, nw) array sharing img's memory."""
+    owner = img
+    while isinstance(owner.base, np.ndarray):
+        owner = owner.base
+    lo, hi = np.lib.array_utils.byte_bounds(owner)
+    p = img.__array_interface__["data"][0]
+    if not owner.flags.c_contiguous or p < lo or p + nh * nw > hi:
+        raise RuntimeError("this strided view, read as nh x nw consecutive bytes from its first element (what the "
+                           "reference's caster does, opencv_type_casters.h:200), would run past its buffer")
+    flat = owner.reshape(-1).view(np.uint8)
+    return flat[p - lo:p - lo + nh * nw].reshape(nh, nw)
 
 
 def keypoint_tuples(kps: np.ndarray) -> list:

@@ -177,3 +177,19 @@ def test_extractor_configurations_bit_exact(ci):
     i, a, b = _first_diff(kps, okps)
     assert i == len(kps), f"{params}: keypoint {i} differs: {a} vs {b}"
     assert np.array_equal(desc, odesc), f"{params}: descriptors differ"
+
+
+def test_strided_view_input_follows_the_reference_caster():
+    """A sliced ROI view is read as nh x nw consecutive bytes from its first element (the reference caster
+    ignores strides, opencv_type_casters.h:200): the drop-in's result equals the oracle's on those bytes and
+    differs from the result on the pixels the view shows (tests/test_input_contract.py pins the bytes)."""
+    img, _ = synth.make_pair(8)
+    v = img[30:330, 150:1000]
+    nh, nw = v.shape
+    first = 30 * img.shape[1] + 150
+    raw = img.reshape(-1)[first:first + nh * nw].reshape(nh, nw).copy()
+    kps, desc = ORBextractor(**KITTI).extract(v)
+    okps, odesc = O.OracleExtractor(**KITTI).extract(raw)
+    assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
+    shown, _ = O.OracleExtractor(**KITTI).extract(np.ascontiguousarray(v))
+    assert shown.tobytes() != kps.tobytes()
