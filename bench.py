@@ -740,7 +740,9 @@ def main():
     c4 = None
     if extras and not strong and not args.no_c4:
         c4_first, c4_n = shard(C4_TOTAL_PAIRS, world, rank)
-        c4_sh = Shard(images[: 2 * c4_n], c4_n, args.streams, dev, args.width, args.height, args.nfeatures)
+        c4_imgs = (images[: 2 * c4_n] if c4_n <= P else  # a small --pairs run: the shard needs its own pairs
+                   torch.from_numpy(synth.make_batch(c4_n, seed0=c4_first, width=args.width, height=args.height)).to(dev))
+        c4_sh = Shard(c4_imgs, c4_n, args.streams, dev, args.width, args.height, args.nfeatures)
         el4 = timed(c4_sh.step, args.steps, args.warmup, dev, world)
         c4 = {"total_pairs": C4_TOTAL_PAIRS, "pairs_per_gpu": c4_n, "handles_per_gpu": len(c4_sh.fes),
               "value": round(C4_TOTAL_PAIRS * args.steps / el4, 2), "unit": "pairs/s",

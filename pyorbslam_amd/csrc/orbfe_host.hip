@@ -96,6 +96,13 @@ struct orbfe_ctx {
 
     hipStream_t own_stream = nullptr;
     bool octree_force = false;  // orbfe_set_octree_kernel(h, 1): the per-candidate k_octree at every geometry
+    // k_resize_cascade strip tables of the reserved geometry, per strip count (resize_strips)
+    struct Cascade {
+        int S = 0, off_b = 0, off_x = 0, lds = 0;
+        DevBuf<int16_t> tab;
+    };
+    std::vector<std::unique_ptr<Cascade>> cascades;
+    int cascade_force = 0;  // orbfe_microbench: 0 automatic, > 0 that strip count, -1 never
     // HIP graphs (orbfe_set_graphs, default on): a batch's or a frame's whole enqueue is captured once per
     // (buffers, arguments) key into an executable graph and replayed with one hipGraphLaunch.  gen counts the
     // reallocations of the handle's buffers / geometry changes, which every key includes; a capture goes on
@@ -298,15 +305,19 @@ void octree_tables(LevelGeo& L, int n_feat, std::vector<uint32_t>& tab) {
     std::vector<int> xc(L.oct_nx);
     for (int x = 0; x < L.oct_nx; ++x) xp[x] = xpath(x, &xc[x]);
     for (int y = 0; y < L.oct_ny; ++y) yp[y] = ypath(y);
-    // least D separating neighbours (paths are monotone in x / y, so neighbours suffice)
+    // least D separating neighbours (paths are monotone in x / y, so neighbours suffice).  Only coordinates
+    // a key can take matter: a FAST cell's keys lie in its ROI minus the 3-px circle border, so x_rel <=
+    // span_x - 4 and y_rel <= span_y - 4 (ORBextractor.cpp:788-824); the table's last entries (which the
+    // float column split can leave outside their column's box, e.g. 2460 px wide, level 5) only clamp.
     int D = 1;
-    for (int x = 1; x < L.oct_nx; ++x)
+    const int kx = std::max(1, L.oct_nx - 4), ky = std::max(1, L.oct_ny - 4);
+    for (int x = 1; x < kx; ++x)
         if (xc[x] == xc[x - 1]) {
             const uint32_t d = xp[x] ^ xp[x - 1];
             if (!d) throw Error(ORBFE_EINVAL, "octree tables: two columns of a level share a path");
             D = std::max(D, kDmax - (31 - __builtin_clz(d)));
         }
-    for (int y = 1; y < L.oct_ny; ++y) {
+    for (int y = 1; y < ky; ++y) {
         const uint32_t d = yp[y] ^ yp[y - 1];
         if (!d) throw Error(ORBFE_EINVAL, "octree tables: two rows share a path");
         D = std::max(D, kDmax - (31 - __builtin_clz(d)));
@@ -560,6 +571,7 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
     if (W != c.W || H != c.H) {
         invalidate_results(c);
         c.drop_graphs();
+        c.cascades.clear();
         build_geometry(c, W, H);
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
@@ -619,8 +631,93 @@ void prof_mark(orbfe_ctx& c, hipStream_t s, int k) {
 
 // Images [i0, i0 + n) of the batch: every per-image buffer is passed at the chunk's offset, the
 // kernels index images from there.  prof: record stage boundaries on s.
+// k_resize_cascade strips (see the kernel): S strips of the top level's rows, and below it, level by level,
+// the rows strip s owns (a partition: the first source row of its next-level rows onwards) and the rows it
+// computes (its own plus the source rows of the next level's computed rows).  Null when the LDS the strips
+// need exceeds 150 KiB.
+std::unique_ptr<orbfe_ctx::Cascade> resize_strips(const orbfe_ctx& c, int S) {
+    const Geo& g = c.geo;
+    const int L = g.nlevels, top = L - 1;
+    if (L < 2 || S < 1 || S > g.lv[top].h) return nullptr;
+    std::vector<std::vector<int>> own(L, std::vector<int>(S + 1)), clo(L, std::vector<int>(S)), chi(L, std::vector<int>(S));
+    for (int k = 0; k <= S; ++k) own[top][k] = (int)((int64_t)k * g.lv[top].h / S);
+    auto yt = [&](int l, int dy) -> const ResizeY& { return c.yt[g.lv[l].ytab_off + dy]; };
+    for (int l = top - 1; l >= 1; --l) {
+        own[l][0] = 0;
+        own[l][S] = g.lv[l].h;
+        for (int k = 1; k < S; ++k) own[l][k] = yt(l + 1, own[l + 1][k]).sy0;
+    }
+    for (int k = 0; k < S; ++k) {
+        clo[top][k] = own[top][k];
+        chi[top][k] = own[top][k + 1];
+        if (chi[top][k] <= clo[top][k]) return nullptr;
+        for (int l = top - 1; l >= 1; --l) {
+            clo[l][k] = std::min(own[l][k], yt(l + 1, clo[l + 1][k]).sy0);
+            chi[l][k] = std::max(own[l][k + 1], yt(l + 1, chi[l + 1][k] - 1).sy1 + 1);
+        }
+    }
+    size_t A = 0, B = 0;
+    std::vector<int16_t> tab((size_t)S * L * 4, 0);
+    for (int k = 0; k < S; ++k) {
+        const int ys_lo = yt(1, clo[1][k]).sy0, ys_hi = yt(1, chi[1][k] - 1).sy1;
+        A = std::max(A, (size_t)(ys_hi - ys_lo + 1) * g.W + 8);  // the staged level-0 run (+ misalignment)
+        for (int l = 1; l < L; ++l) {
+            const size_t b = (size_t)(chi[l][k] - clo[l][k]) * g.lv[l].pitch;
+            (l & 1 ? B : A) = std::max(l & 1 ? B : A, b);
+            int16_t* e = &tab[((size_t)k * L + l) * 4];
+            e[0] = (int16_t)clo[l][k];
+            e[1] = (int16_t)chi[l][k];
+            e[2] = (int16_t)own[l][k];
+            e[3] = (int16_t)own[l][k + 1];
+        }
+    }
+    auto a16 = [](size_t v) { return (v + 16 + 15) & ~(size_t)15; };  // + the taps' 12-byte over-read
+    std::unique_ptr<orbfe_ctx::Cascade> cs(new orbfe_ctx::Cascade());
+    cs->S = S;
+    cs->off_b = (int)a16(A);
+    cs->off_x = cs->off_b + (int)a16(B);
+    cs->lds = cs->off_x + (int)((size_t)g.rs_ngrp * 36);
+    if (cs->lds > 150 * 1024) return nullptr;
+    cs->tab.ensure(tab.size());
+    HIPCK(hipMemcpy(cs->tab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+    HIPCK(prepare_resize_cascade(cs->lds));
+    return cs;
+}
+
+// Pyramid of an n-image enqueue: the one-launch cascade for small batches (< kCascadeImages images; strips
+// for >= ~512 workgroups, at least 3 top-level rows each), else the per-level k_resize_rows launches.  Built
+// (uploads, kernel attributes) before an enqueue is captured: prepare_pyramid runs outside the capture.
+constexpr int kCascadeImages = 32;
+
+int cascade_strips(const orbfe_ctx& c, int n) {
+    if (c.cascade_force) return c.cascade_force;
+    if (n >= kCascadeImages || c.geo.nlevels < 2) return -1;
+    const int htop = c.geo.lv[c.geo.nlevels - 1].h;
+    return std::max(4, std::min((512 + n - 1) / n, std::max(4, htop / 3)));
+}
+
+orbfe_ctx::Cascade* find_cascade(orbfe_ctx& c, int S) {
+    for (auto& cs : c.cascades)
+        if (cs->S == S) return cs.get();
+    return nullptr;
+}
+
+void prepare_pyramid(orbfe_ctx& c, int n) {
+    for (int S = cascade_strips(c, n); S > 0 && !find_cascade(c, S); S += 4) {  // more strips need less LDS
+        std::unique_ptr<orbfe_ctx::Cascade> cs = resize_strips(c, S);
+        if (cs) {
+            c.cascades.push_back(std::move(cs));
+            return;
+        }
+        if (S > c.geo.lv[c.geo.nlevels - 1].h) return;
+    }
+}
+
+// zero_ovf: the batch's overflow word is cleared by the first pyramid launch instead of a separate memset
+// (one stream operation less in front of the chain); only for an enqueue that owns the word alone (not the
+// concurrent chunks of orbfe_set_lanes, one of which could clear a bound another chunk already flagged).
 void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int n, hipStream_t s, bool prof,
-                   int lane = -1) {
+                   int lane = -1, bool zero_ovf = false) {
     const Geo& g = c.geo;
     const uint8_t* in = d_in + (int64_t)i0 * pitch;
     uint8_t* ws = c.d_ws.p + (int64_t)i0 * g.ws_bytes;
@@ -634,7 +731,18 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     uint8_t* desc = c.d_desc.p + (int64_t)i0 * g.kp_cap * 32;
     int* count = c.d_count.p + i0;
     if (prof) prof_mark(c, s, 0);
-    for (int l = 1; l < g.nlevels; ++l) HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s));
+    if (zero_ovf && g.nlevels < 2) HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
+    int S = cascade_strips(c, n);
+    orbfe_ctx::Cascade* cs = nullptr;
+    while (S > 0 && !(cs = find_cascade(c, S)) && S <= g.lv[g.nlevels - 1].h) S += 4;  // prepare_pyramid's choice
+    if (cs) {
+        HIPCK(launch_resize_cascade(g, in, pitch, ws, c.d_xt.p, c.d_yt.p, cs->tab.p, cs->S, cs->off_b, cs->off_x, cs->lds,
+                                    n, s, zero_ovf ? c.d_overflow.p : nullptr));
+    } else {
+        for (int l = 1; l < g.nlevels; ++l)
+            HIPCK(launch_resize(g, l, in, pitch, ws, c.d_xt.p, c.d_yt.p, n, s, 0,
+                                zero_ovf && l == 1 ? c.d_overflow.p : nullptr));
+    }
     if (prof) prof_mark(c, s, 1);
     (void)lane;
     if (g.ncells > 0) HIPCK(launch_detect(g, c.d_cells.p, in, pitch, ws, cell_count, slots, n, s));
@@ -655,8 +763,8 @@ void check_extract(orbfe_ctx& c, int64_t pitch, int n) {
 void enqueue_extract(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n, hipStream_t s) {
     if (n <= 0) return;
     check_extract(c, pitch, n);
-    HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
-    extract_range(c, d_in, pitch, 0, n, s, true);
+    prepare_pyramid(c, n);
+    extract_range(c, d_in, pitch, 0, n, s, true, -1, true);
     c.last_in = d_in;
     c.last_pitch = pitch;
     c.last_images = n;
@@ -783,10 +891,10 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     check_extract(c, pitch, 2 * n_pairs);
     const int K = std::max(1, std::min(c.lanes, n_pairs));
     if (K == 1) {
+        prepare_pyramid(c, 2 * n_pairs);
         run_enqueue(c, {1, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx)}, s,
                     [&](hipStream_t q) {
-                        HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), q));
-                        extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true);
+                        extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true, -1, true);
                         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, q);
                         prof_mark(c, q, 5);
                     });
@@ -802,6 +910,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
         HIPCK(hipEventRecord(c.lane_fork, s));
         for (int k = 0; k < K; ++k) {
             const int p0 = (int)((int64_t)n_pairs * k / K), p1 = (int)((int64_t)n_pairs * (k + 1) / K);
+            prepare_pyramid(c, 2 * (p1 - p0));
             hipStream_t ls = c.lane_stream[k];
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
             extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k);
@@ -999,10 +1108,10 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
         const std::vector<uint64_t> key = {2, bits_of(h->h_in.p), bits_of(h->d_in.p), bits_of(hb),
                                            bits_of(want_pyramid ? h->d_shear.p : nullptr), (uint64_t)width,
                                            (uint64_t)height, bits_of(bf), bits_of(fx), (uint64_t)o};
+        prepare_pyramid(*h, 2);
         run_enqueue(*h, key, s, [&](hipStream_t q) {
             HIPCK(hipMemcpyAsync(h->d_in.p, h->h_in.p, (size_t)pitch + (size_t)width * height, hipMemcpyHostToDevice, q));
-            HIPCK(hipMemsetAsync(h->d_overflow.p, 0, sizeof(int), q));
-            extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, false);
+            extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, -1, true);
             stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q);
             if (want_pyramid) HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, q));
             auto d2h = [&](size_t off, const void* src, size_t bytes) {
@@ -1550,8 +1659,26 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
         auto run = [&] {
             switch (stage) {
                 case 0:
+                    // variant 6: the one-launch cascade with the automatic strip count for this batch, 100 + S:
+                    // with S strips (tools/microbench.py); 7: the per-level launches whatever the batch size
+                    if (variant == 6 || variant >= 100) {
+                        orbfe_ctx::Cascade* cs = nullptr;
+                        for (int S = variant >= 100 ? variant - 100 : cascade_strips(*h, n); S > 0; S += 4) {
+                            if (!(cs = find_cascade(*h, S))) {
+                                std::unique_ptr<orbfe_ctx::Cascade> ns = resize_strips(*h, S);
+                                if (ns) h->cascades.push_back(std::move(ns));
+                                cs = find_cascade(*h, S);
+                            }
+                            if (cs || S > g.lv[g.nlevels - 1].h) break;
+                        }
+                        if (!cs) throw Error(ORBFE_EINVAL, "no cascade strip count fits the LDS");
+                        HIPCK(launch_resize_cascade(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p,
+                                                    cs->tab.p, cs->S, cs->off_b, cs->off_x, cs->lds, n, s));
+                        break;
+                    }
                     for (int l = 1; l < g.nlevels; ++l)
-                        HIPCK(launch_resize(g, l, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, n, s, variant));
+                        HIPCK(launch_resize(g, l, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, n, s,
+                                            variant == 7 ? 0 : variant));
                     break;
                 case 1:
                     HIPCK(launch_detect(g, h->d_cells.p, h->last_in, h->last_pitch, h->d_ws.p, h->d_cell_count.p,

@@ -60,14 +60,21 @@ struct UndistortArgs {
 };
 hipError_t launch_undistort(const float* xy_in, int n, int stride_in, float* xy_out, const UndistortArgs& a,
                             hipStream_t s);
+// zero_word (optional): a device int the launch sets to 0 (the batch's overflow word, cleared without a memset)
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
-                         const ResizeY* yt, int n_images, hipStream_t s, int variant = 0);
+                         const ResizeY* yt, int n_images, hipStream_t s, int variant = 0, int* zero_word = nullptr);
 hipError_t launch_detect(const Geo& g, const CellGeo* cells, const uint8_t* in, int64_t in_pitch, const uint8_t* ws,
                          int* cell_count, uint32_t* slots, int n_images, hipStream_t s, int variant = 0,
                          int* stats = nullptr);
 size_t octree_lds_bytes(const Geo& g, int maxcell);
 size_t octree_bins_lds_bytes(const Geo& g, int maxcell);
 size_t detect_lds_bytes(const Geo& g);
+// k_resize_cascade (all levels in one launch, small batches): strips = n_strips x nlevels x {computed lo, hi,
+// owned lo, hi} int16 (host resize_strips); LDS: buffer A at 0, B at off_b, the x selectors at off_x
+hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
+                                 const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
+                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word = nullptr);
+hipError_t prepare_resize_cascade(int lds_bytes);
 // raise the octree kernels' dynamic-LDS attribute for this geometry (outside any stream capture)
 hipError_t prepare_octree(const Geo& g, int maxcell);
 // Geo::oct_v selects k_octree_bins (0) or the per-candidate pass kernel k_octree (1); octab: the

@@ -300,7 +300,8 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 // and 64-bit store address are gone).  Blocks of 256 <= 64 W_g R_s <= 512 threads (the host picks R_s).
 __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                      uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
-                                                     const ResizeY* __restrict__ yt, int wg, int remw, int wgl) {
+                                                     const ResizeY* __restrict__ yt, int wg, int remw, int wgl,
+                                                     int* __restrict__ zero_word) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     uint32_t* s_src = (uint32_t*)rs_lds;  // staged source rows
     const LevelGeo& L = g.lv[l];
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     int bx, img;
     xcd_block(bx, img);
     const int t = threadIdx.x, nthr = blockDim.x;
+    if (zero_word && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) *zero_word = 0;
     const int dy0 = bx * kRsRows, nrow = min(kRsRows, L.h - dy0);
     const int ngrp = (L.w + 3) >> 2;
     int sstride;
@@ -415,6 +417,138 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         ch += ch_step;
         if (ch >= ch_end) return;
         chunk(ch);
+    }
+}
+
+// k_resize_cascade: the whole pyramid (levels 1 .. L-1) in ONE launch for small batches, where the seven
+// per-level launches are seven latency chains of a few microseconds each (8 pairs: 58 us of 233 per step).
+// One 512-thread workgroup per (horizontal strip, image).  Strip s computes at every level the rows the
+// next level's rows of the strip need (its own rows, plus a halo its neighbours also compute) and stores
+// the rows it owns; ownership partitions every level (host: resize_strips), so each output row is written
+// exactly once, with the arithmetic of k_resize_rows (same taps, same vertical rounding).  Level 0's source
+// rows are staged from the input like k_resize_rows; every later level reads the previous level's strip
+// from LDS, ping-ponging between two buffers (A: level 0 staging and even levels, B: odd levels).
+// tab: per (strip, level) int16 {computed lo, hi, owned lo, hi}; offB / offX: byte offsets of buffer B and
+// of the per-level x selector table in the dynamic LDS.
+__global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+                                                        uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
+                                                        const ResizeY* __restrict__ yt, const int16_t* __restrict__ tab,
+                                                        int offB, int offX, int* __restrict__ zero_word) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    typedef __attribute__((address_space(3))) uint32_t lds_w32;
+    const int strip = blockIdx.x, img = blockIdx.y, t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), nwv = blockDim.x >> 6;
+    if (zero_word && strip == 0 && img == 0 && t == 0) *zero_word = 0;
+    const int L = g.nlevels;
+    const int16_t* st = tab + (int64_t)strip * L * 4;
+    const uint32_t baseA = (uint32_t)(uintptr_t)(lds_u32*)rs_lds;
+    const uint32_t baseB = baseA + (uint32_t)offB;
+    uint4* s_xa = (uint4*)(rs_lds + offX);  // per group: v_perm selectors, then (a0, a1) weights
+    int* s_sx0 = (int*)(s_xa + 2 * g.rs_ngrp);  // per group: its first source column
+    // ---- level 0 rows the strip's level 1 needs, staged as a flat dword run (k_resize_rows' staging)
+    uint32_t src_base = baseA, src_sh;
+    int src_row0, src_stride;
+    {
+        const LevelGeo& L1 = g.lv[1];
+        const ResizeY* yb = yt + L1.ytab_off;
+        const int c0 = st[4], c1 = st[5];
+        const int ys_lo = yb[c0].sy0, ys_hi = yb[c1 - 1].sy1;
+        const uintptr_t a0 = (uintptr_t)(in + (int64_t)img * in_pitch + (int64_t)ys_lo * g.W);
+        src_sh = (uint32_t)(a0 & 3);
+        const uint32_t* gsrc = (const uint32_t*)(a0 - src_sh);
+        const int ndw = ((ys_hi - ys_lo) * g.W + g.W + (int)src_sh + 3) >> 2;
+        uint32_t* s_src = (uint32_t*)rs_lds;
+        for (int base = 0; base < ndw; base += 512 * kRsSlots / 2) {
+            uint32_t v[kRsSlots / 2];
+#pragma unroll
+            for (int k = 0; k < kRsSlots / 2; ++k) {
+                const int i = base + t + 512 * k;
+                v[k] = i < ndw ? gsrc[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kRsSlots / 2; ++k) {
+                const int i = base + t + 512 * k;
+                if (i < ndw) s_src[i] = v[k];
+            }
+        }
+        src_row0 = ys_lo;
+        src_stride = g.W;
+    }
+    for (int l = 1; l < L; ++l) {
+        const LevelGeo& Lv = g.lv[l];
+        const int c0 = st[4 * l], c1 = st[4 * l + 1], o0 = st[4 * l + 2], o1 = st[4 * l + 3];
+        const int ngrp = (Lv.w + 3) >> 2, nch = (ngrp + 63) >> 6;
+        // x selectors / weights of the level (k_resize's per-group form)
+        const uint4* xg = (const uint4*)(xt + Lv.xtab_off);
+        for (int gi = t; gi < ngrp; gi += blockDim.x) {
+            const uint4 q0 = xg[2 * gi], q1 = xg[2 * gi + 1];
+            auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
+            s_xa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+            s_xa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
+            s_sx0[gi] = (int)q0.x;
+        }
+        const uint32_t dst_base = (l & 1) ? baseB : baseA;
+        __syncthreads();  // selectors staged; the source rows complete (previous level / staging)
+        const ResizeY* yb = yt + Lv.ytab_off;
+        uint8_t* gdst = ws + (int64_t)img * g.ws_bytes + Lv.ws_off;
+        const int pitch = Lv.pitch;
+        // items (row, chunk), row-major; wave wv takes items wv, wv + nwv, ...: row / chunk advanced
+        // incrementally (uniform), no division per item
+        const int nitems = (c1 - c0) * nch;
+        int r = c0 + wv / nch, ch = wv - (wv / nch) * nch;
+        const int step_r = nwv / nch, step_c = nwv - step_r * nch;
+        for (int item = wv; item < nitems; item += nwv) {
+            const int grp = ch * 64 + lane;
+            if (grp < ngrp) {
+                const uint4 e = s_xa[2 * grp], aa = s_xa[2 * grp + 1];
+                const int sx0 = s_sx0[grp];
+                const ResizeY y = yb[r];
+                const uint32_t lsrc = src_base + src_sh + (uint32_t)sx0;
+                const uint32_t r0 = (uint32_t)((y.sy0 - src_row0) * src_stride), r1 = (uint32_t)((y.sy1 - src_row0) * src_stride);
+                const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
+                auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
+                    const uint32_t A = lsrc + roff, o = A & 3u;
+                    lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
+                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                    const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+                    h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
+                                                  __builtin_bit_cast(us2, aa.x), 0u, false);
+                    h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
+                                                  __builtin_bit_cast(us2, aa.y), 0u, false);
+                    h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
+                                                  __builtin_bit_cast(us2, aa.z), 0u, false);
+                    h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                                  __builtin_bit_cast(us2, aa.w), 0u, false);
+                };
+                uint32_t h0[4], h1[4];
+                taps(r0, h0);
+                taps(r1, h1);
+                const int dx = 4 * grp;
+                uint32_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
+                if (dx + 3 >= Lv.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (dx + k >= Lv.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+                }
+                const uint32_t px = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+                *(lds_w32*)(uintptr_t)(dst_base + (uint32_t)((r - c0) * pitch + dx)) = px;
+                if (r >= o0 && r < o1) *(uint32_t*)(gdst + (int64_t)r * pitch + dx) = px;  // pitch padding past w
+            }
+            r += step_r;
+            ch += step_c;
+            if (ch >= nch) {
+                ch -= nch;
+                ++r;
+            }
+        }
+        src_base = dst_base;
+        src_sh = 0;
+        src_row0 = c0;
+        src_stride = pitch;
+        __syncthreads();  // this level's rows complete before the next level reads them / the selectors change
     }
 }
 
@@ -2456,8 +2590,10 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // [floor(y - 2s), ceil(y + 2s)] (double arithmetic, s = scale of its octave).  One workgroup per pair:
 // LDS histogram -> block scan -> fill.  The order inside a bucket is irrelevant: k_stereo reduces
 // (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
-// Also writes the compact (x, octave) record of every right keypoint.
-__global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
+// Also writes the compact (x, octave) record of every right keypoint.  1 024 threads: the kernel is one
+// latency chain per pair (load, count, scan, fill), so small batches (a frame's one pair) wait on it whole.
+constexpr int kBkThreads = 1024;
+__global__ __launch_bounds__(kBkThreads) void k_stereo_bucket(Geo g, StereoArgs A) {
     extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
     __shared__ int scan_tmp[257];
     const int pr = blockIdx.x, t = threadIdx.x;
@@ -2469,9 +2605,9 @@ __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
     // per-octave scales in LDS: a lane-indexed read of the kernel argument would be a vector memory load
     __shared__ float s_scale[kMaxLevels];
     if (t < kMaxLevels) s_scale[t] = g.scale[t];
-    for (int i = t; i <= H; i += 256) cnt[i] = 0;
+    for (int i = t; i <= H; i += kBkThreads) cnt[i] = 0;
     __syncthreads();
-    for (int i = t; i < nR; i += 256) {
+    for (int i = t; i < nR; i += kBkThreads) {
         const orbfe_keypoint kr = KR[i];
         rinfo[i] = make_float2(kr.x, __int_as_float(kr.octave));
         const double r = 2.0 * (double)s_scale[kr.octave];
@@ -2482,9 +2618,9 @@ __global__ __launch_bounds__(256) void k_stereo_bucket(Geo g, StereoArgs A) {
     const int total = block_excl_scan(cnt, H, scan_tmp);
     if (t == 0) cnt[H] = total;
     __syncthreads();
-    for (int i = t; i <= H; i += 256) off[i] = cnt[i];
+    for (int i = t; i <= H; i += kBkThreads) off[i] = cnt[i];
     __syncthreads();
-    for (int i = t; i < nR; i += 256) {
+    for (int i = t; i < nR; i += kBkThreads) {
         const orbfe_keypoint kr = KR[i];
         const double r = 2.0 * (double)s_scale[kr.octave];
         const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
@@ -2833,7 +2969,7 @@ __global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restric
 
 // ------------------------------------------------------------------------------- launchers
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
-                         const ResizeY* yt, int n_images, hipStream_t s, int variant) {
+                         const ResizeY* yt, int n_images, hipStream_t s, int variant, int* zero_word) {
     dim3 grid((g.lv[l].h + kRsRows - 1) / kRsRows, n_images);
     const LevelGeo& L = g.lv[l];  // LDS sized for this level (tables + its bands' source rows)
     // production: k_resize_rows (profiles/r03/resize_rows_ab_r3f.log: 414 -> 394 us per 256 pairs
@@ -2852,7 +2988,7 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
         const int threads = 64 * (wgl * sets + remw);
         if (threads < 256 || threads > 512) return hipErrorInvalidConfiguration;
         hipLaunchKernelGGL(k_resize_rows, grid, dim3(threads), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in, in_pitch,
-                           ws, xt, yt, wg, remw, wgl);
+                           ws, xt, yt, wg, remw, wgl, zero_word);
         return hipGetLastError();
     }
 #ifdef ORBFE_DEV_VARIANTS
@@ -2931,7 +3067,18 @@ size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
 // process and kernel, when a geometry is built (orbfe_host.hip prepare_kernels): launches, which may be
 // inside a graph capture, only check.
 static int g_lds_attr[2] = {64 * 1024, 64 * 1024};  // k_octree_bins, k_octree
+static int g_lds_cascade = 64 * 1024;                // k_resize_cascade
 static std::mutex g_lds_mu;
+
+hipError_t prepare_resize_cascade(int lds_bytes) {
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    if (lds_bytes <= g_lds_cascade) return hipSuccess;
+    if (lds_bytes > 160 * 1024) return hipErrorInvalidValue;
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)k_resize_cascade, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e == hipSuccess) g_lds_cascade = lds_bytes;
+    return e;
+}
 
 hipError_t prepare_octree(const Geo& g, int maxcell) {
     const size_t need[2] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell)};
@@ -2944,6 +3091,16 @@ hipError_t prepare_octree(const Geo& g, int maxcell) {
         g_lds_attr[k] = (int)need[k];
     }
     return hipSuccess;
+}
+
+hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
+                                 const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
+                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word) {
+    if (g.nlevels < 2 || n_images <= 0) return hipSuccess;
+    if (lds_bytes > g_lds_cascade) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
+    hipLaunchKernelGGL(k_resize_cascade, dim3(n_strips, n_images), dim3(512), (size_t)lds_bytes, s, g, in, in_pitch, ws,
+                       xt, yt, strips, off_b, off_x, zero_word);
+    return hipGetLastError();
 }
 
 hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_count, const uint32_t* slots,
@@ -3012,7 +3169,7 @@ hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const u
 }
 
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
-    hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);
+    hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(kBkThreads), (size_t)4 * (g.H + 1), s, g, a);
     hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 15) / 16, n_pairs), dim3(256), 0, s, g, a);
     return hipGetLastError();
 }

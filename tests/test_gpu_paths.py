@@ -111,19 +111,36 @@ def test_stress_images_bit_exact(name):
     assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
 
 
-def test_fast_lattice_takes_the_one_pass_path_and_stays_in_capacity():
-    """The lattice fills every cell with candidates at both thresholds: more than half of a cell's pairs
-    pass at minTh, so the two queues meet and the cell takes the one-pass path (orbfe_debug_detect_stats),
-    and the overflow word stays 0 (no on-device capacity bound is reached)."""
+def _detect_stats(img_pair):
     torch = pytest.importorskip("torch")
     from pyorbslam_amd.batch import StereoFrontEnd
-    img = _stress_images()["lattice"]
     fe = StereoFrontEnd(max_pairs=1, lanes=1)
-    fe.enqueue(torch.from_numpy(np.stack([img, img])).cuda(), 1)
-    assert fe.overflow() == 0
+    fe.enqueue(torch.from_numpy(np.stack(img_pair)).cuda(), 1)
+    ovf = fe.overflow()
     st = (C.c_int64 * 3)()
     call("orbfe_debug_detect_stats", fe.handle, st)
-    assert st[0] > 0 and st[1] > 0, list(st)
+    return fe, ovf, list(st)
+
+
+def test_fast_lattice_stays_in_capacity():
+    """The densest lattice of isolated corners: every candidate a cell can hold under the strict NMS
+    (slot_cap) and the octree's equal-score ties; the overflow word stays 0 and the result is bit-exact."""
+    img = _stress_images()["lattice"]
+    fe, ovf, st = _detect_stats((img, img))
+    assert ovf == 0 and st[0] == 2 * 1220, st
+    kl, dl = fe.fetch_image(0)
+    okl, odl = O.OracleExtractor(**KITTI).extract(img)
+    assert kl.tobytes() == okl.tobytes() and np.array_equal(dl, odl)
+
+
+def test_noise_takes_the_one_pass_path():
+    """Uniform noise passes the cardinal pre-test at both thresholds almost everywhere, so a cell's minTh
+    queue (from the front) and iniTh queue (from the back) meet and the cell takes k_detect's one-pass path
+    (both thresholds over the minTh queue; orbfe_debug_detect_stats[1]); bit-exact against the oracle."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (376, 1241)).astype(np.uint8)
+    fe, ovf, st = _detect_stats((img, img))
+    assert ovf == 0 and st[1] > st[0] // 2, st
     kl, dl = fe.fetch_image(0)
     okl, odl = O.OracleExtractor(**KITTI).extract(img)
     assert kl.tobytes() == okl.tobytes() and np.array_equal(dl, odl)
@@ -131,13 +148,8 @@ def test_fast_lattice_takes_the_one_pass_path_and_stays_in_capacity():
 
 def test_natural_images_take_the_two_queue_path():
     """On the synthetic KITTI image no cell's queues meet; most cells fall back to minTh."""
-    torch = pytest.importorskip("torch")
-    from pyorbslam_amd.batch import StereoFrontEnd
-    fe = StereoFrontEnd(max_pairs=1, lanes=1)
-    fe.enqueue(torch.from_numpy(synth.make_batch(1, seed0=0)).cuda(), 1)
-    st = (C.c_int64 * 3)()
-    call("orbfe_debug_detect_stats", fe.handle, st)
-    assert st[0] == 2 * 1220 and st[1] == 0 and st[2] > st[0] // 3, list(st)
+    _, ovf, st = _detect_stats(tuple(synth.make_batch(1, seed0=0)))
+    assert ovf == 0 and st[0] == 2 * 1220 and st[1] == 0 and st[2] > st[0] // 3, st
 
 
 NAMES = ["kitti", "euroc", "noise", "patch", "lattice", "corner"]
@@ -218,3 +230,30 @@ def test_graph_stereo_against_restatement_after_replays():
         sa, va = stereo_oracle.encode(a)
         sb, vb = stereo_oracle.encode(b)
         assert np.array_equal(sa, sb) and np.array_equal(va, vb)
+
+
+@pytest.mark.parametrize("shape,params", [((376, 1241), KITTI), ((480, 752), EUROC), ((333, 641), KITTI),
+                                          ((157, 211), dict(KITTI, nfeatures=500)), ((400, 2560), KITTI),
+                                          ((376, 1241), dict(KITTI, scaleFactor=1.1, nlevels=12))])
+def test_resize_cascade_equals_per_level_launches(shape, params):
+    """k_resize_cascade (the one-launch pyramid of small batches, strips with halo rows) against the
+    per-level k_resize_rows launches and the oracle, at several strip counts (orbfe_microbench stage 0:
+    variant 7 = per-level, 100 + S = the cascade with S strips)."""
+    h, w = shape
+    img = synth.make_pair(31, w, h)[0]
+    ex = ORBextractor(**params)
+    ex.extract(img)  # one image: the cascade path
+    auto = ex.GetImagePyramid(sheared=False)
+    orc = O.OracleExtractor(**params)
+    orc.extract(img)
+    for l, (g, o) in enumerate(zip(auto, orc.pyramid())):
+        assert np.array_equal(g, o), f"cascade level {l}"
+    ms = C.c_float()
+    call("orbfe_microbench", ex.handle, 0, 7, 1, C.byref(ms))
+    for l, (g, o) in enumerate(zip(ex.GetImagePyramid(sheared=False), orc.pyramid())):
+        assert np.array_equal(g, o), f"per-level level {l}"
+    top_h = orc.pyramid()[-1].shape[0]
+    for S in sorted({1, 2, 5, max(1, top_h // 3), top_h}):
+        call("orbfe_microbench", ex.handle, 0, 100 + S, 1, C.byref(ms))
+        for l, (g, o) in enumerate(zip(ex.GetImagePyramid(sheared=False), orc.pyramid())):
+            assert np.array_equal(g, o), f"cascade S={S} level {l}"
