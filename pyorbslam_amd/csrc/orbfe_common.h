@@ -64,6 +64,9 @@ struct CellGeo {
 #define ORBFE_RS_ROWS 16  // experiment switch (tools/dbg/build_variant.sh)
 #endif
 constexpr int kRsRows = ORBFE_RS_ROWS;  // k_resize output rows per workgroup (band)
+// batches of fewer images than this run the small-batch (latency) variants: the one-launch pyramid cascade,
+// one FAST cell per wave, 1 024-thread octree workgroups
+constexpr int kSmallBatchImages = 32;
 // k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
 constexpr int kOctKeys = 7424;
 

@@ -687,7 +687,7 @@ std::unique_ptr<orbfe_ctx::Cascade> resize_strips(const orbfe_ctx& c, int S) {
 // Pyramid of an n-image enqueue: the one-launch cascade for small batches (< kCascadeImages images; strips
 // for >= ~512 workgroups, at least 3 top-level rows each), else the per-level k_resize_rows launches.  Built
 // (uploads, kernel attributes) before an enqueue is captured: prepare_pyramid runs outside the capture.
-constexpr int kCascadeImages = 32;
+constexpr int kCascadeImages = kSmallBatchImages;
 
 int cascade_strips(const orbfe_ctx& c, int n) {
     if (c.cascade_force) return c.cascade_force;
@@ -1103,6 +1103,8 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
         if (want_pyramid) h->d_shear.ensure(2 * (size_t)g.shear_bytes);
         const uint8_t* pair[2] = {left, right};
         stage_host(*h, pair, 2, width, height, stride, pitch);
+        uint8_t* hb_dev = nullptr;  // the frame buffer as the device addresses it (k_copy_segments writes it)
+        HIPCK(hipHostGetDevicePointer((void**)&hb_dev, hb, 0));
         // everything after the host copy is one enqueue (a graph replay when graphs are on): both images in,
         // the 2-image pipeline, stereo, optionally the sheared views, every result out to pinned memory
         const std::vector<uint64_t> key = {2, bits_of(h->h_in.p), bits_of(h->d_in.p), bits_of(hb),
@@ -1114,18 +1116,22 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
             extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, -1, true);
             stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q);
             if (want_pyramid) HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, q));
-            auto d2h = [&](size_t off, const void* src, size_t bytes) {
-                HIPCK(hipMemcpyAsync(hb + off, src, bytes, hipMemcpyDeviceToHost, q));
+            // every result into the page-locked frame buffer with ONE kernel's stores over PCIe (k_copy_segments;
+            // 8-9 copy-engine transfers cost ~60 us per frame in fixed costs, rocprof round 4)
+            CopySegs cp{};
+            auto seg = [&](size_t off, const void* src, size_t bytes) {
+                cp.seg[cp.n++] = {(const uint32_t*)src, (uint32_t*)(hb_dev + off), (uint32_t)((bytes + 3) / 4)};
             };
-            d2h(h->fo_ovf, h->d_overflow.p, sizeof(int));
-            d2h(h->fo_count, h->d_count.p, 2 * sizeof(int));
-            d2h(h->fo_kps, h->d_kps.p, 2 * cap * sizeof(orbfe_keypoint));
-            d2h(h->fo_desc, h->d_desc.p, 2 * cap * 32);
-            d2h(h->fo_uR, h->d_uR.p, cap * sizeof(float));
-            d2h(h->fo_depth, h->d_depth.p, cap * sizeof(float));
-            d2h(h->fo_status, h->d_status.p, cap);
-            d2h(h->fo_match, h->d_match.p, cap * sizeof(int32_t));
-            if (want_pyramid) d2h(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
+            seg(h->fo_ovf, h->d_overflow.p, sizeof(int));
+            seg(h->fo_count, h->d_count.p, 2 * sizeof(int));
+            seg(h->fo_kps, h->d_kps.p, 2 * cap * sizeof(orbfe_keypoint));
+            seg(h->fo_desc, h->d_desc.p, 2 * cap * 32);
+            seg(h->fo_uR, h->d_uR.p, cap * sizeof(float));
+            seg(h->fo_depth, h->d_depth.p, cap * sizeof(float));
+            seg(h->fo_status, h->d_status.p, cap);
+            seg(h->fo_match, h->d_match.p, cap * sizeof(int32_t));
+            if (want_pyramid) seg(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
+            HIPCK(launch_copy_segments(cp, q));
         });
         HIPCK(hipStreamSynchronize(s));
         h->last_in = h->d_in.p;

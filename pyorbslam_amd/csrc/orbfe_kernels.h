@@ -53,6 +53,16 @@ struct PackArgs {
 };
 
 hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s);
+// k_copy_segments: up to 12 dword copies in one launch (dst may be device-visible page-locked host memory)
+struct CopySegs {
+    struct Seg {
+        const uint32_t* src;
+        uint32_t* dst;
+        uint32_t dwords;
+    } seg[12];
+    int n;
+};
+hipError_t launch_copy_segments(const CopySegs& a, hipStream_t s);
 // k_undistort: pinhole K (float in the reference: mK is float32) + distortion (k1, k2, p1, p2[, k3])
 struct UndistortArgs {
     double fx, fy, cx, cy;

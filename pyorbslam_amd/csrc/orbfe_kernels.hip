@@ -1630,7 +1630,10 @@ __host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB
     return o;
 }
 
-__global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
+// NT threads: 256 (large batches: the workgroups of many images share the CUs) or 1 024 for small batches,
+// where one image's level-0 workgroup is the critical path and its key sweeps take 4x fewer rounds.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
                                                             const int* __restrict__ cell_count,
                                                             const uint32_t* __restrict__ slots,
                                                             const uint32_t* __restrict__ octab,
@@ -1683,13 +1686,13 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     const int D = L.oct_d, D0 = L.oct_d0, B = L.oct_bins, bsh = 2 * (D - D0);
     const int nx = L.oct_nx, ny = L.oct_ny;
     // ---- 1. per-cell key offsets (cell order = vToDistributeKeys order), the level's tables, empty bins
-    for (int i = t; i < ncell; i += kObThreads) {
+    for (int i = t; i < ncell; i += NT) {
         d.coff[i] = cell_count[(int64_t)img * g.ncells + L.cell0 + i];
         d.soff[i] = cells[L.cell0 + i].slot_off;
     }
-    for (int i = t; i < nx + ny; i += kObThreads) d.tab[i] = octab[L.oct_xt + i];  // X then Y (adjacent)
-    for (int i = t; i <= B; i += kObThreads) d.bins[i] = 0;
-    for (int i = t; i < B; i += kObThreads) d.bmax[i] = 0;
+    for (int i = t; i < nx + ny; i += NT) d.tab[i] = octab[L.oct_xt + i];  // X then Y (adjacent)
+    for (int i = t; i <= B; i += NT) d.bins[i] = 0;
+    for (int i = t; i < B; i += NT) d.bmax[i] = 0;
     __syncthreads();
     mark(3);
     if (t < 64) {
@@ -1709,7 +1712,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     // first cell of every 64-key block: the cells whose key range holds a multiple of 64 (keys past the
     // table's Geo::oct_kblk_max blocks start from its last entry and walk further)
     const int nblk = g.oct_kblk_max;
-    for (int c = t; c < ncell; c += kObThreads) {
+    for (int c = t; c < ncell; c += NT) {
         const int a = d.coff[c], e = d.coff[c + 1];
         for (int b = (a + 63) >> 6; (b << 6) < e && b < nblk; ++b) d.bcell[b] = (uint16_t)c;
     }
@@ -1754,7 +1757,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
         }
     };
     mark(5);
-    for_keys(t, kObThreads, [&](int k, uint32_t v, uint32_t cd) {
+    for_keys(t, NT, [&](int k, uint32_t v, uint32_t cd) {
         bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
     });
     mark(6);
@@ -2061,7 +2064,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     const uint8_t* dep = s_cur ? d.dep1 : d.dep0;
     uint32_t* best = (uint32_t*)d.sa;
     // a node of depth <= D0 covers whole bins: its best key is the maximum of their maxima
-    for (int p = t; p < S; p += kObThreads) {
+    for (int p = t; p < S; p += NT) {
         const int dp = dep[p];
         const int lo = (int)(code[p] >> bsh);
         uint32_t m = 0u;
@@ -2074,11 +2077,11 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
     __syncthreads();
     // nodes deeper than D0 (rare): a sweep over the keys of their bins (bin flag, then a prefix match)
     if (nd > 0) {
-        for (int i = t; i < nd; i += kObThreads) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
+        for (int i = t; i < nd; i += NT) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
         __syncthreads();
     }
     if (nd > 0)
-        for_keys(t, kObThreads, [&](int kk, uint32_t v, uint32_t cd) {
+        for_keys(t, NT, [&](int kk, uint32_t v, uint32_t cd) {
             if (kk >= K || d.bins[cd >> bsh] != kObDeep) return;
             for (int i = 0; i < nd; ++i) {
                 const int q = d.dl[i];
@@ -2089,7 +2092,7 @@ __global__ __launch_bounds__(kObThreads) void k_octree_bins(Geo g, const CellGeo
             }
         });
     __syncthreads();
-    for (int p = t; p < S; p += kObThreads) {
+    for (int p = t; p < S; p += NT) {
         const uint32_t bv = best[p];
         const int k = 0xFFFFFF - (int)(bv & 0xFFFFFFu);
         if (bv != 0u && k < K) {
@@ -3012,7 +3015,9 @@ size_t detect_lds_bytes(const Geo& g) {
 int detect_cpw(const Geo& g, int n_images, int variant) {
     if (variant == 4) return 4;
     if (variant == 5) return 1;
-    return (int64_t)n_images * ((g.ncells + kFdCells - 1) / kFdCells) < 8 * 256 ? 1 : kFdCells;
+    // 8 pairs: 39 us with one cell per wave against 47 with four (tools/microbench.py, round 4)
+    return n_images < kSmallBatchImages || (int64_t)n_images * ((g.ncells + kFdCells - 1) / kFdCells) < 8 * 256 ? 1
+                                                                                                                : kFdCells;
 }
 
 template <int RP, int NS>
@@ -3066,7 +3071,7 @@ size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
 // gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB on request.  Raised (never lowered) once per
 // process and kernel, when a geometry is built (orbfe_host.hip prepare_kernels): launches, which may be
 // inside a graph capture, only check.
-static int g_lds_attr[2] = {64 * 1024, 64 * 1024};  // k_octree_bins, k_octree
+static int g_lds_attr[3] = {64 * 1024, 64 * 1024, 64 * 1024};  // k_octree_bins<256>, k_octree, k_octree_bins<1024>
 static int g_lds_cascade = 64 * 1024;                // k_resize_cascade
 static std::mutex g_lds_mu;
 
@@ -3081,10 +3086,10 @@ hipError_t prepare_resize_cascade(int lds_bytes) {
 }
 
 hipError_t prepare_octree(const Geo& g, int maxcell) {
-    const size_t need[2] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell)};
-    const void* fn[2] = {(const void*)k_octree_bins, (const void*)k_octree};
+    const size_t need[3] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell), octree_bins_lds_bytes(g, maxcell)};
+    const void* fn[3] = {(const void*)k_octree_bins<kObThreads>, (const void*)k_octree, (const void*)k_octree_bins<1024>};
     std::lock_guard<std::mutex> lk(g_lds_mu);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 3; ++k) {
         if ((int)need[k] <= g_lds_attr[k] || need[k] > 160 * 1024) continue;
         const hipError_t e = hipFuncSetAttribute(fn[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[k]);
         if (e != hipSuccess) return e;
@@ -3108,9 +3113,15 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
     if (g.oct_v == 0) {
         const size_t lds = octree_bins_lds_bytes(g, maxcell);
-        if ((int)lds > g_lds_attr[0]) return hipErrorInvalidConfiguration;  // prepare_octree was not run
-        hipLaunchKernelGGL(k_octree_bins, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells, cell_count, slots,
-                           octab, lvl_kp, lvl_count, overflow, maxcell, prof);
+        if ((int)lds > g_lds_attr[0] || (int)lds > g_lds_attr[2]) return hipErrorInvalidConfiguration;  // prepare_octree
+        // 1 024 threads for small batches (variant 1 / 2 force 256 / 1 024, tools/microbench.py)
+        const bool wide = variant == 2 || (variant != 1 && n_images < kSmallBatchImages);
+        if (wide)
+            hipLaunchKernelGGL(k_octree_bins<1024>, dim3(n_images, g.nlevels), dim3(1024), lds, s, g, cells, cell_count,
+                               slots, octab, lvl_kp, lvl_count, overflow, maxcell, prof);
+        else
+            hipLaunchKernelGGL(k_octree_bins<kObThreads>, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells,
+                               cell_count, slots, octab, lvl_kp, lvl_count, overflow, maxcell, prof);
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
@@ -3216,6 +3227,24 @@ hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, 
     const int64_t items = 2 + (int64_t)a.kp_cap * 31;
     const unsigned bx = (unsigned)std::min<int64_t>((items + 255) / 256, 64);
     hipLaunchKernelGGL(k_pack, dim3(bx, n_pairs), dim3(256), 0, s, a, out, pair0);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------- k_copy_segments
+// Several dword-aligned device -> (device-visible page-locked host) copies in one launch: the per-frame path's
+// results go to the host as one kernel's stores over PCIe instead of eight copy-engine transfers of a few
+// microseconds of fixed cost each.  blockIdx.y = segment.
+__global__ __launch_bounds__(256) void k_copy_segments(CopySegs a) {
+    const CopySegs::Seg sg = a.seg[blockIdx.y];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < sg.dwords; i += gridDim.x * 256u) sg.dst[i] = sg.src[i];
+}
+
+hipError_t launch_copy_segments(const CopySegs& a, hipStream_t s) {
+    if (a.n <= 0) return hipSuccess;
+    uint32_t most = 0;
+    for (int k = 0; k < a.n; ++k) most = std::max(most, a.seg[k].dwords);
+    const unsigned bx = std::max(1u, std::min((most + 1023u) / 1024u, 32u));
+    hipLaunchKernelGGL(k_copy_segments, dim3(bx, a.n), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 """Per-step view of a rocprofv3 kernel trace of tools/small_trace.py: kernels grouped into steps (a step
-starts at each k_resize_rows of level 1, i.e. every 7th resize dispatch), per step the span from the first
+starts at each k_resize_cascade, or at every 7th k_resize_rows dispatch, i.e. level 1), per step the span from the first
 kernel's start to the last one's end, the summed kernel time and the idle gaps; per kernel the median
 duration.  usage: python tools/ktrace_steps.py TRACE_DIR [skip_steps]"""
 import collections
@@ -20,11 +20,11 @@ def main():
     rows.sort()
     steps, cur, nres = [], [], 0
     for s, e, n in rows:
-        if n in ("k_resize_rows",):
-            if nres % 7 == 0 and cur:
+        if n == "k_resize_rows" or n == "k_resize_cascade":
+            if (n == "k_resize_cascade" or nres % 7 == 0) and cur:
                 steps.append(cur)
                 cur = []
-            nres += 1
+            nres += n == "k_resize_rows"
         cur.append((s, e, n))
     if cur:
         steps.append(cur)
