@@ -663,8 +663,19 @@ def main():
                     help="host-fed records via a device buffer + D2H copy instead of k_pack into pinned host memory")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 tracking-loop latency (N = 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 EuRoC line (N = 1, KITTI runs only)")
+    ap.add_argument("--allow-dev-env", action="store_true",
+                    help="run with ORBFE_* development variables set (A/B of library builds); value is then null")
     args = ap.parse_args()
 
+    # no development switch may change what is measured unnoticed: ORBFE_* variables other than the rank
+    # backend choice are recorded in the line, and a run with one set prints no value
+    orbfe_env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("ORBFE_")}
+    dev_env = {k: v for k, v in orbfe_env.items() if k != "ORBFE_DIST_BACKEND"}
+    if dev_env and not args.allow_dev_env:
+        print(json.dumps({"error": f"ORBFE_* development variables set ({', '.join(dev_env)}): unset them (they select "
+                                   "another library build; --allow-dev-env runs anyway and reports value null)"}),
+              flush=True)
+        raise SystemExit(2)
     wr = check_world(args)
     if wr is None:
         raise SystemExit(launch_ranks(args))
@@ -790,7 +801,7 @@ def main():
         cam, cam_name = CAMERAS.get((args.width, args.height), ("custom", f"{args.width}x{args.height}"))
         workload = workload_name(args.width, args.height, args.nfeatures, P, args.total_pairs if strong else 0)
         out = {"metric": f"stereo pairs/s (ORB extract L+R + stereo match), {cam_name}, 1/2/4/8 GPU"}
-        if elapsed is not None:
+        if elapsed is not None and not dev_env:
             pairs_per_s = total * args.steps / elapsed
             out.update({"value": round(pairs_per_s, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
                         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4)})
@@ -807,8 +818,10 @@ def main():
                                        f"{P} pairs per GPU on {world} GPU(s)")
                        + " (independent ranks, no data-path collective)",
                        "handles_per_gpu": n_handles, "lanes_per_handle": args.lanes},
-            "build_id": build,
+            "build_id": build, "orbfe_env": orbfe_env,
         })
+        if dev_env and elapsed is not None:
+            out["dev_env_ms_per_step"] = round(elapsed / args.steps * 1e3, 4)
         if parity is not None:
             out.update(parity)
         if stage_ms:

@@ -176,13 +176,18 @@ int orbfe_frontend_batch_device(orbfe_handle h, const uint8_t* d_images, int64_t
  * their layout do not depend on it. */
 int orbfe_set_lanes(orbfe_handle h, int32_t lanes);
 
-/* orbfe_set_graphs: 1 (default) = orbfe_frontend_batch_device (one lane) and orbfe_frame_extract run their
- * whole enqueue (12-16 kernels, memsets and copies) as a HIP graph, captured on the first call with a given
+/* orbfe_set_graphs(mask): which enqueues run as a HIP graph, captured on the first call with a given
  * (buffers, pointers, sizes, bf, fx) key and replayed with one hipGraphLaunch afterwards (up to 8 cached
- * graphs per handle, dropped when the handle's buffers are reallocated); 0 = launch every operation on the
- * stream.  Results do not depend on it.  Profiling (orbfe_profile_begin) always takes the stream path.
- * orbfe_graph_stats: captures and graph launches so far, graphs cached now (any pointer may be NULL). */
-int orbfe_set_graphs(orbfe_handle h, int32_t on);
+ * graphs per handle, dropped when the handle's buffers are reallocated): ORBFE_GRAPH_FRAME =
+ * orbfe_frame_extract (default: the per-frame path runs on one stream, a graph saves its launches),
+ * ORBFE_GRAPH_BATCH = orbfe_frontend_batch_device with one lane (off by default: graph launches of handles on
+ * different streams measured to serialise their chains, 0.27 -> 0.40 ms for 8 pairs as 4 handles).  0 =
+ * every operation launched on the stream.  Results do not depend on it; profiling (orbfe_profile_begin)
+ * always takes the stream path.  orbfe_graph_stats: captures and graph launches so far, graphs cached now
+ * (any pointer may be NULL). */
+#define ORBFE_GRAPH_FRAME 1
+#define ORBFE_GRAPH_BATCH 2
+int orbfe_set_graphs(orbfe_handle h, int32_t mask);
 int orbfe_graph_stats(orbfe_handle h, int64_t* captures, int64_t* launches, int32_t* cached);
 
 /* Device result layout of the last batch (pointers into handle-owned device memory):

@@ -30,7 +30,7 @@ def camera_constants(width: int, height: int) -> tuple[float, float]:
 class StereoFrontEnd:
     def __init__(self, width: int = 1241, height: int = 376, max_pairs: int = 64, nfeatures: int = 2000,
                  scaleFactor: float = 1.2, nlevels: int = 8, iniThFAST: int = 20, minThFAST: int = 7,
-                 resize_simd_lanes: int = 16, lanes: int = 4, graphs: bool = True):
+                 resize_simd_lanes: int = 16, lanes: int = 4, graphs: bool = False):
         self.width, self.height, self.max_pairs = int(width), int(height), int(max_pairs)
         self._params = _lib.make_params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes)
         h = C.c_void_p()
@@ -39,8 +39,9 @@ class StereoFrontEnd:
         call("orbfe_batch_reserve", h, self.width, self.height, 2 * self.max_pairs)
         # concurrent chunks of enqueue() on internal streams (results are independent of it)
         call("orbfe_set_lanes", h, int(lanes))
-        # one-lane enqueues replay a captured HIP graph (orbfe_set_graphs; results do not depend on it)
-        call("orbfe_set_graphs", h, int(bool(graphs)))
+        # graphs=True: one-lane enqueues replay a captured HIP graph (orbfe_set_graphs ORBFE_GRAPH_BATCH; off by
+        # default: graph launches on several streams serialise the handles' chains; results do not depend on it)
+        call("orbfe_set_graphs", h, 3 if graphs else 1)
         v = BatchView()
         call("orbfe_batch_view_get", h, C.byref(v))
         self.kp_cap = v.kp_cap

@@ -107,7 +107,7 @@ struct orbfe_ctx {
     // (buffers, arguments) key into an executable graph and replayed with one hipGraphLaunch.  gen counts the
     // reallocations of the handle's buffers / geometry changes, which every key includes; a capture goes on
     // cap_stream, so the caller's stream only ever sees the launches.
-    bool use_graphs = true;
+    int graph_mask = ORBFE_GRAPH_FRAME;  // orbfe_set_graphs: which enqueues replay graphs
     uint64_t gen = 0;
     hipStream_t cap_stream = nullptr;
     struct GraphEntry {
@@ -846,8 +846,8 @@ uint64_t bits_of(const void* p) { return (uint64_t)(uintptr_t)p; }
 // on the first use of the key, replayed with one hipGraphLaunch afterwards.  Every pointer and argument
 // the enqueue bakes into its launches must be part of the key (c.gen stands for the handle's buffers).
 template <class F>
-void run_enqueue(orbfe_ctx& c, std::vector<uint64_t> key, hipStream_t s, F&& enqueue) {
-    if (!c.use_graphs || c.prof_on) {
+void run_enqueue(orbfe_ctx& c, int kind, std::vector<uint64_t> key, hipStream_t s, F&& enqueue) {
+    if (!(c.graph_mask & kind) || c.prof_on) {
         enqueue(s);
         return;
     }
@@ -892,7 +892,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
     const int K = std::max(1, std::min(c.lanes, n_pairs));
     if (K == 1) {
         prepare_pyramid(c, 2 * n_pairs);
-        run_enqueue(c, {1, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx)}, s,
+        run_enqueue(c, ORBFE_GRAPH_BATCH, {1, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx)}, s,
                     [&](hipStream_t q) {
                         extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true, -1, true);
                         stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, q);
@@ -1111,7 +1111,7 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
                                            bits_of(want_pyramid ? h->d_shear.p : nullptr), (uint64_t)width,
                                            (uint64_t)height, bits_of(bf), bits_of(fx), (uint64_t)o};
         prepare_pyramid(*h, 2);
-        run_enqueue(*h, key, s, [&](hipStream_t q) {
+        run_enqueue(*h, ORBFE_GRAPH_FRAME, key, s, [&](hipStream_t q) {
             HIPCK(hipMemcpyAsync(h->d_in.p, h->h_in.p, (size_t)pitch + (size_t)width * height, hipMemcpyHostToDevice, q));
             extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, -1, true);
             stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q);
@@ -1769,11 +1769,12 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
     });
 }
 
-int orbfe_set_graphs(orbfe_handle h, int32_t on) {
+int orbfe_set_graphs(orbfe_handle h, int32_t mask) {
     return guarded([&] {
         if (!h) throw Error(ORBFE_EINVAL, "null handle");
-        h->use_graphs = on != 0;
-        if (!h->use_graphs) h->drop_graphs();
+        if (mask & ~(ORBFE_GRAPH_FRAME | ORBFE_GRAPH_BATCH)) throw Error(ORBFE_EINVAL, "unknown graph flags");
+        h->graph_mask = mask;
+        h->drop_graphs();
     });
 }
 

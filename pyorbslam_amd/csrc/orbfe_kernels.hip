@@ -376,13 +376,16 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         const int dx = 4 * grp;
         const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
         const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-        auto row = [&](int rr) {
+        // source rows of a derived level sit a multiple of 4 bytes apart (16-byte pitch): a lane's byte offset
+        // inside the dword is then the same in every row (aligned = true: no per-row address masking)
+        const uint32_t o_inv = lsrc & 3u, a_inv = lsrc - o_inv;
+        auto row = [&](int rr, auto aligned) {
             const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
             const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
             const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
             auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
-                const uint32_t A = lsrc + roff, o = A & 3u;
-                lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
+                const uint32_t o = decltype(aligned)::value ? o_inv : (lsrc + roff) & 3u;
+                lds_u32* w = (lds_u32*)(uintptr_t)(decltype(aligned)::value ? a_inv + roff : lsrc + roff - o);
                 const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
                 const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
                 h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
@@ -409,10 +412,11 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
                                                   (uint32_t)(rr * L.pitch), 0);
         };
-        if (!remwave) {
-            for (int rr = set; rr < nrow; rr += nset) row(rr);
+        const int r_first = remwave ? row0 : set, r_step = remwave ? rstep : nset;
+        if ((sstride & 3) == 0) {
+            for (int rr = r_first; rr < nrow; rr += r_step) row(rr, std::true_type{});
         } else {
-            for (int rr = row0; rr < nrow; rr += rstep) row(rr);
+            for (int rr = r_first; rr < nrow; rr += r_step) row(rr, std::false_type{});
         }
         ch += ch_step;
         if (ch >= ch_end) return;

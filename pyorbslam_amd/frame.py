@@ -98,6 +98,11 @@ def extract_orb(self, flag, image) -> None:
         else:
             self.mvKeys_, self.mDescriptors = left.operator_kd(image)
         self.mvKeys = [KeyPoint(*kp) for kp in self.mvKeys_]
+        if isinstance(left, ORBextractor) and len(left.last_keypoints) == len(self.mvKeys):
+            # the keypoints' pt as doubles straight from the extractor's float32 fields (the values the
+            # KeyPoints were built from), for assign_features_to_grid while mvKeys is still this list
+            kl = left.last_keypoints
+            self._orbfe_kxy = (self.mvKeys, np.stack((kl["x"], kl["y"]), axis=1).astype(np.float64))
     elif flag == 1:
         pend = right.take_pending(image) if isinstance(right, ORBextractor) else None
         if pend is not None:
@@ -230,7 +235,11 @@ def assign_features_to_grid(self) -> None:
         if ref is None:
             raise RuntimeError("install() did not record the reference assign_features_to_grid")
         return ref(self)
-    pts = np.fromiter((c for kp in kps for c in kp.pt), np.float64, count=2 * n).reshape(n, 2)
+    kxy = getattr(self, "_orbfe_kxy", None)
+    if kxy is not None and kxy[0] is kps and len(kxy[1]) == n:
+        pts = kxy[1]  # extract_orb's copy of the same coordinates (mvKeys is the list it built)
+    else:
+        pts = np.fromiter((c for kp in kps for c in kp.pt), np.float64, count=2 * n).reshape(n, 2)
     px = np.round((pts[:, 0] - self.mnMinX) * self.mfGridElementWidthInv).astype(int)
     py = np.round((pts[:, 1] - self.mnMinY) * self.mfGridElementHeightInv).astype(int)
     cols, rows = self.FRAME_GRID_COLS, self.FRAME_GRID_ROWS

@@ -6,7 +6,7 @@ args=$1; shift
 for round in 1 2; do
   for lib in "" "$@"; do
     if [ -n "$lib" ]; then export ORBFE_LIB=pyorbslam_amd/_lib/variants/$lib/liborbfe.so; else unset ORBFE_LIB; fi
-    v=$(timeout -k 10 150 python bench.py $args --cpu-sample 0 2>/dev/null | tail -1 | python -c "import sys,json; print(json.loads(sys.stdin.read())['value'])") || exit 1
+    v=$(timeout -k 10 150 python bench.py $args --cpu-sample 0 --allow-dev-env 2>/dev/null | tail -1 | python -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'] or round(d['config']['total_pairs_per_step'] / d['dev_env_ms_per_step'] * 1e3, 1))") || exit 1
     echo "round $round lib ${lib:-HEAD-tree} [$args] -> $v"
   done
 done
