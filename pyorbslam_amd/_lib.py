@@ -152,6 +152,12 @@ def call(name: str, *args) -> None:
     check(name, getattr(lib(), name)(*args))
 
 
+def has(name: str) -> bool:
+    """Whether the loaded library exports `name` (always true for the in-tree build, which must export every
+    declared symbol; an older build under ORBFE_LIB A/B may predate some)."""
+    return getattr(lib(), name, None) is not None
+
+
 def ptr(a: np.ndarray | None) -> C.c_void_p | None:
     return None if a is None else C.c_void_p(a.ctypes.data)
 

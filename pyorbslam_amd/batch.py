@@ -41,7 +41,8 @@ class StereoFrontEnd:
         call("orbfe_set_lanes", h, int(lanes))
         # graphs=True: one-lane enqueues replay a captured HIP graph (orbfe_set_graphs ORBFE_GRAPH_BATCH; off by
         # default: graph launches on several streams serialise the handles' chains; results do not depend on it)
-        call("orbfe_set_graphs", h, 3 if graphs else 1)
+        if _lib.has("orbfe_set_graphs"):
+            call("orbfe_set_graphs", h, 3 if graphs else 1)
         v = BatchView()
         call("orbfe_batch_view_get", h, C.byref(v))
         self.kp_cap = v.kp_cap
@@ -78,6 +79,8 @@ class StereoFrontEnd:
     def graph_stats(self) -> dict:
         """HIP-graph captures and launches of this handle so far, and the graphs cached now."""
         cap, lau, n = C.c_int64(), C.c_int64(), C.c_int32()
+        if not _lib.has("orbfe_graph_stats"):
+            return {"captures": 0, "launches": 0, "cached": 0}
         call("orbfe_graph_stats", self._h, C.byref(cap), C.byref(lau), C.byref(n))
         return {"captures": cap.value, "launches": lau.value, "cached": n.value}
 

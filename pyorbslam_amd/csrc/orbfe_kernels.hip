@@ -298,6 +298,7 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
 // y table, the store is a buffer store with the row offset in soffset: per 4 pixels only the taps, the
 // vertical rounding and the pack are VALU work (k_resize's per-item row / table LDS reads, index wrap
 // and 64-bit store address are gone).  Blocks of 256 <= 64 W_g R_s <= 512 threads (the host picks R_s).
+template <bool MULTI>
 __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                      uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                      const ResizeY* __restrict__ yt, int wg, int remw, int wgl,
@@ -376,16 +377,13 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         const int dx = 4 * grp;
         const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
         const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-        // source rows of a derived level sit a multiple of 4 bytes apart (16-byte pitch): a lane's byte offset
-        // inside the dword is then the same in every row (aligned = true: no per-row address masking)
-        const uint32_t o_inv = lsrc & 3u, a_inv = lsrc - o_inv;
-        auto row = [&](int rr, auto aligned) {
+        auto row = [&](int rr) {
             const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
             const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
             const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
             auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
-                const uint32_t o = decltype(aligned)::value ? o_inv : (lsrc + roff) & 3u;
-                lds_u32* w = (lds_u32*)(uintptr_t)(decltype(aligned)::value ? a_inv + roff : lsrc + roff - o);
+                const uint32_t A = lsrc + roff, o = A & 3u;
+                lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
                 const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
                 const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
                 h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
@@ -412,12 +410,12 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
                                                   (uint32_t)(rr * L.pitch), 0);
         };
-        const int r_first = remwave ? row0 : set, r_step = remwave ? rstep : nset;
-        if ((sstride & 3) == 0) {
-            for (int rr = r_first; rr < nrow; rr += r_step) row(rr, std::true_type{});
+        if (!remwave) {
+            for (int rr = set; rr < nrow; rr += nset) row(rr);
         } else {
-            for (int rr = r_first; rr < nrow; rr += r_step) row(rr, std::false_type{});
+            for (int rr = row0; rr < nrow; rr += rstep) row(rr);
         }
+        if (!MULTI) return;  // one chunk per wave (every level up to 2 048 px): round 3's code exactly
         ch += ch_step;
         if (ch >= ch_end) return;
         chunk(ch);
@@ -668,7 +666,7 @@ __host__ __device__ inline int detect_roi_elems(const Geo& g, int rp) {
 // 5 waves per SIMD (<= 96 VGPRs; 4 for the wider / taller ROI variants, which need the registers) and
 // <= 8 KiB of LDS for KITTI / EuRoC cells: detect is bound by how many
 // cells are in flight per CU (16 -> 10 resident waves costs +32 %, tools/microbench.py variant 8).
-template <int V, int RP, int NS, int CPW>
+template <int V, int RP, int NS, int CPW, bool ST = false>
 __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(Geo g, const CellGeo* __restrict__ cells, const uint8_t* __restrict__ in,
                                                int64_t in_pitch, const uint8_t* __restrict__ ws,
                                                int* __restrict__ cell_count, uint32_t* __restrict__ slots,
@@ -950,7 +948,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
         };
         const bool collide = npq + npa > cap;
         // orbfe_debug_detect_stats: cells that took the one-pass path despite two thresholds (the queues met)
-        if (stats && lane == 0 && two && collide) atomicAdd(&stats[1], 1);
+        if (ST && lane == 0 && two && collide) atomicAdd(&stats[1], 1);
         int total = 0;
         if (two && !collide) {
             int t0, t1;
@@ -962,7 +960,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             nms_stage(pq + cap - 1, -1, nna, max(g.ini_th, 1), 0, t0, t1);
             total = t0;
             if (t0 == 0) {  // minTh fallback: every pair of B (the A pairs' M is recomputed, identically)
-                if (stats && lane == 0) atomicAdd(&stats[2], 1);
+                if (ST && lane == 0) atomicAdd(&stats[2], 1);
                 const int nnb = m_stage(pq, 1, npq, max(g.min_th, 1));
                 nms_stage(pq, 1, nnb, max(g.min_th, 1), 0, t0, t1);
                 total = t0;
@@ -987,7 +985,7 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
             }
         }
         if (lane == 0) cell_count[(int64_t)img * g.ncells + c] = min(total, cg.slot_cap);
-        if (stats && lane == 0) atomicAdd(&stats[0], 1);
+        if (ST && lane == 0) atomicAdd(&stats[0], 1);
         };
         process();
         __syncthreads();  // the next cell overwrites the ROI and the M map
@@ -2994,8 +2992,11 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
         const int sets = std::max(1, (4 - remw + wgl - 1) / wgl);  // >= 256 threads per block (the staging threads)
         const int threads = 64 * (wgl * sets + remw);
         if (threads < 256 || threads > 512) return hipErrorInvalidConfiguration;
-        hipLaunchKernelGGL(k_resize_rows, grid, dim3(threads), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in, in_pitch,
-                           ws, xt, yt, wg, remw, wgl, zero_word);
+        // MULTI: a wave walks several 64-group chunks (levels wider than 2 048 px); the one-chunk form is
+        // instantiated apart (the loop around it cost 3 % on KITTI, tools/dbg/mb_ab.sh, round 4)
+        auto k = wg > wgl ? k_resize_rows<true> : k_resize_rows<false>;
+        hipLaunchKernelGGL(k, grid, dim3(threads), (size_t)L.rs_nsrc * L.rs_sp + 16, s, g, l, in, in_pitch, ws, xt, yt, wg,
+                           remw, wgl, zero_word);
         return hipGetLastError();
     }
 #ifdef ORBFE_DEV_VARIANTS
@@ -3037,7 +3038,8 @@ static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* 
            : variant == 3 ? k_detect<3, RP, NS, kFdCells> : cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>;
 #else
     const size_t lds = detect_lds_bytes(g);
-    auto k = cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>;
+    auto k = stats ? (cpw == 1 ? k_detect<0, RP, NS, 1, true> : k_detect<0, RP, NS, kFdCells, true>)  // debug counters
+                   : (cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>);
 #endif
     hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots, stats);
 }
