@@ -408,13 +408,14 @@ def max_over_ranks(v, dev, world):
     return float(t.item())
 
 
-def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True) -> dict:
+def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = False, h2d_streams: int = 1,
+             records: bool = True) -> dict:
     """The shard's pairs streamed from pinned host memory every step, per handle: its images H2D on a copy
     stream into one of two device buffers (the handle starts as soon as ITS chunk has landed, while the
-    next chunks are still on the link), its batch, and its pairs' records back in pinned host memory —
-    zero_copy (default): k_pack writes them straight into the pinned buffer over PCIe (device-visible
-    hipHostMalloc memory, no device staging buffer and no copy-engine transfer competing with the H2D
-    copies); otherwise packed into device memory and copied D2H on a second copy stream.  Timed like a step
+    next chunks are still on the link), its batch, and its pairs' records back in pinned host memory:
+    packed into device memory and copied D2H on a second copy stream (default), or with zero_copy k_pack
+    writes them straight into the pinned buffer over PCIe — measured slower, 47.3 k vs 51.1 k pairs/s
+    same-box (round 4): the CUs' PCIe stores slow the H2D copies more than a copy-engine transfer does.  Timed like a step
     (barrier + synchronize, max over ranks); the records of the last step are checked against the handles'
     own results."""
     import torch
@@ -424,10 +425,15 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True)
     H = len(sh.fes)
     hin = torch.from_numpy(host).pin_memory()
     dbuf = [torch.empty(hin.shape, dtype=torch.uint8, device=dev) for _ in range(2)]
-    rb = D.record_bytes(sh.fes[0].kp_cap)
+    # compact records (k_pack_compact, 8 + 91 kp_cap bytes instead of 8 + 121 kp_cap) on the copy path;
+    # the zero-copy variant writes full records (k_pack accepts page-locked host memory)
+    kc = sh.fes[0].kp_cap
+    rb = D.record_bytes(kc) if zero_copy else D.compact_record_bytes(kc)
+    pack_fn = "orbfe_batch_pack_device" if zero_copy else "orbfe_batch_pack_compact_device"
     drec = [] if zero_copy else [torch.empty((n, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
     hrec = [torch.empty((n, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
-    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    h2ds = [torch.cuda.Stream(dev) for _ in range(max(1, h2d_streams))]  # handle j's images on h2ds[j % n]
+    d2h = torch.cuda.Stream(dev)
     ev = {name: [[torch.cuda.Event() for _ in range(H)] for _ in range(2)] for name in ("in", "free", "out")}
     offs = np.concatenate([[0], np.cumsum(sh.counts)]).tolist()
     it = [0]
@@ -438,19 +444,21 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True)
         it[0] += 1
         for j, (f, st, c) in enumerate(zip(sh.fes, sh.streams, sh.counts)):
             o0, o1 = offs[j], offs[j + 1]
+            h2d = h2ds[j % len(h2ds)]
             with torch.cuda.stream(h2d):
                 if seen[b]:
                     h2d.wait_event(ev["free"][b][j])   # handle j finished reading dbuf[b] two steps ago
                 dbuf[b][2 * o0:2 * o1].copy_(hin[2 * o0:2 * o1], non_blocking=True)
                 ev["in"][b][j].record(h2d)
             st.wait_event(ev["in"][b][j])
-            if seen[b] and not zero_copy:
+            if seen[b] and not zero_copy and records:
                 st.wait_event(ev["out"][b][j])         # drec[b] rows of handle j have left the device
             f.enqueue(dbuf[b][2 * o0:2 * o1], c, sh.bf, sh.fx, stream_ptr=st.cuda_stream)
-            dst = hrec[b][o0] if zero_copy else drec[b][o0]
-            call("orbfe_batch_pack_device", f.handle, C.c_void_p(dst.data_ptr()), rb, 0, c, C.c_void_p(st.cuda_stream))
+            if records:
+                dst = hrec[b][o0] if zero_copy else drec[b][o0]
+                call(pack_fn, f.handle, C.c_void_p(dst.data_ptr()), rb, 0, c, C.c_void_p(st.cuda_stream))
             ev["free"][b][j].record(st)
-            if not zero_copy:
+            if not zero_copy and records:
                 with torch.cuda.stream(d2h):
                     d2h.wait_event(ev["free"][b][j])
                     hrec[b][o0:o1].copy_(drec[b][o0:o1], non_blocking=True)
@@ -458,12 +466,19 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True)
         seen[b] = True
 
     el = timed(step, steps, warmup, dev, world)
+    if not records:  # the images' H2D leg and the compute only: what the link allows without the results
+        return {"value": round(world * n * steps / el, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
+                "h2d_GBs_per_gpu": round(host.nbytes * steps / el / 1e9, 2)}
     last = (it[0] - 1) % 2
-    u = D.unpack(sh.fes[0].kp_cap, hrec[last][0].numpy())
+    r0 = hrec[last][0].numpy()
+    u = D.unpack(kc, r0) if zero_copy else D.unpack_compact(kc, r0, sh.fes[0].scales)
     k, d = sh.fes[0].fetch_image(0)
+    kr, dr = sh.fes[0].fetch_image(1)
     s = sh.fes[0].fetch_stereo(0)
     ok = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
-          and np.array_equal(u["u_right"], s["u_right"]))
+          and u["kps_right"].tobytes() == kr.tobytes() and np.array_equal(u["desc_right"], dr)
+          and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["depth"], s["depth"])
+          and np.array_equal(u["status"], s["status"]))
     if not ok:
         raise RuntimeError("host-fed record of pair 0 differs from the handle's own results")
     in_b = host.nbytes
@@ -473,7 +488,9 @@ def host_fed(sh: Shard, host, dev, world, steps, warmup, zero_copy: bool = True)
             "h2d_bytes_per_pair": int(in_b // n), "d2h_bytes_per_pair": int(rb),
             "h2d_GBs_per_gpu": round(in_b * steps / el / 1e9, 2), "d2h_GBs_per_gpu": round(out_b * steps / el / 1e9, 2),
             "pcie_bound_pairs_per_s_per_gpu": round(PCIE_PEAK_GBS * 1e9 / (in_b / n), 1),
-            "record_check": ok, "records": "k_pack into pinned host memory" if zero_copy else "k_pack + D2H copy",
+            "record_check": ok,
+            "records": "k_pack into pinned host memory" if zero_copy else "k_pack_compact + D2H copy (compact records)",
+            "h2d_streams": len(h2ds),
             "what": "per handle: its images H2D from pinned host memory (copy stream, two device buffers), its batch, "
                     "its pairs' records packed " + ("by k_pack straight into pinned host memory (zero-copy stores over "
                                                     "PCIe)" if zero_copy else "on the device and copied D2H (second "
@@ -659,8 +676,10 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="skip the timed rank-0 gather (N > 1)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (64 pairs in total) line")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed (PCIe-inclusive) line")
-    ap.add_argument("--host-fed-copy", action="store_true",
-                    help="host-fed records via a device buffer + D2H copy instead of k_pack into pinned host memory")
+    ap.add_argument("--host-fed-h2d-streams", type=int, default=1, help="copy streams carrying the host-fed H2D chunks")
+    ap.add_argument("--host-fed-zero-copy", action="store_true",
+                    help="host-fed records written by k_pack straight into pinned host memory (default: device buffer "
+                         "+ D2H copy)")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 tracking-loop latency (N = 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 EuRoC line (N = 1, KITTI runs only)")
     ap.add_argument("--allow-dev-env", action="store_true",
@@ -770,7 +789,9 @@ def main():
     # ---- host-fed (PCIe-inclusive) rate of the same workload
     hf = None
     if extras and not args.no_host_fed:
-        hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2, zero_copy=not args.host_fed_copy)
+        hf = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2, zero_copy=args.host_fed_zero_copy,
+                      h2d_streams=args.host_fed_h2d_streams)
+        hf["images_only"] = host_fed(sh, host, dev, world, max(args.steps // 2, 4), 2, records=False)
 
     # ---- C4's rank share (8 pairs) on this GPU, and C5 (EuRoC), N = 1
     share = None

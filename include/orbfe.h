@@ -224,6 +224,15 @@ int orbfe_batch_status(orbfe_handle h, int32_t* overflow);
  * (hipHostMalloc): the records then go over PCIe straight into host memory (no device staging buffer, no
  * copy-engine transfer); pageable memory is refused with ORBFE_EINVAL. */
 int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes);
+/* Compact records (the host-fed D2H leg and the rank-0 gather, 25 % smaller): counts L, R (2 x i32) |
+ * keypoints L, R (kp_cap x {u32 x | y << 12 | octave << 24 in the keypoint's level pixels, f32 angle}) |
+ * descriptors L, R (kp_cap x 32 B) | u_right, depth (kp_cap x f32) | FAST scores L, R (kp_cap x u8) | status
+ * (kp_cap x i8), padded to 16 bytes (8 + 91 kp_cap).  The keypoint tuples follow exactly: x = f32(level x) *
+ * scale[octave] (ORBextractor.cpp:1094-1099), size = (float)(int)(31 * scale[octave]), response = score
+ * (pyorbslam_amd.dist.unpack_compact).  Device memory only. */
+int orbfe_batch_compact_record_bytes(orbfe_handle h, int64_t* bytes);
+int orbfe_batch_pack_compact_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0,
+                                    int32_t n_pairs, void* hip_stream);
 int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0, int32_t n_pairs,
                             void* hip_stream);
 

@@ -73,6 +73,8 @@ SIGNATURES = {
     "orbfe_batch_status": [C.c_void_p, C.POINTER(C.c_int32)],
     "orbfe_batch_record_bytes": [C.c_void_p, C.POINTER(C.c_int64)],
     "orbfe_batch_pack_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p],
+    "orbfe_batch_compact_record_bytes": [C.c_void_p, C.POINTER(C.c_int64)],
+    "orbfe_batch_pack_compact_device": [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p],
     "orbfe_batch_fetch": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_batch_fetch_stereo": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                  C.POINTER(C.c_int32)],

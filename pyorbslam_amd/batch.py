@@ -46,6 +46,8 @@ class StereoFrontEnd:
         v = BatchView()
         call("orbfe_batch_view_get", h, C.byref(v))
         self.kp_cap = v.kp_cap
+        self.scales = np.zeros(int(nlevels), np.float32)  # the level scale factors (compact records)
+        call("orbfe_get_scales", h, self.scales.ctypes.data_as(C.c_void_p), None, None, None, None)
 
     def __del__(self):
         h = getattr(self, "_h", None)

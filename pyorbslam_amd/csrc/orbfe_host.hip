@@ -1371,6 +1371,39 @@ int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_byte
     });
 }
 
+int64_t compact_record_bytes(int kp_cap) { return (8 + 91 * (int64_t)kp_cap + 15) / 16 * 16; }
+
+int orbfe_batch_compact_record_bytes(orbfe_handle h, int64_t* bytes) {
+    return guarded([&] {
+        if (!h || !bytes) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->W <= 0) throw Error(ORBFE_ESTATE, "call orbfe_batch_reserve first");
+        *bytes = compact_record_bytes(h->geo.kp_cap);
+    });
+}
+
+int orbfe_batch_pack_compact_device(orbfe_handle h, uint8_t* d_records, int64_t rec_bytes, int32_t pair0,
+                                    int32_t n_pairs, void* hip_stream) {
+    return guarded([&] {
+        if (!h || !d_records) throw Error(ORBFE_EINVAL, "null argument");
+        if (pair0 < 0 || n_pairs < 0 || pair0 + n_pairs > h->last_pairs)
+            throw Error(ORBFE_EINVAL, "pair range outside the last stereo batch");
+        if (rec_bytes != compact_record_bytes(h->geo.kp_cap))
+            throw Error(ORBFE_EINVAL, "record size does not match kp_cap");
+        if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
+        hipPointerAttribute_t pa{};
+        if (hipPointerGetAttributes(&pa, d_records) != hipSuccess || pa.type != hipMemoryTypeDevice) {
+            (void)hipGetLastError();
+            throw Error(ORBFE_EINVAL, "compact records must be device memory");
+        }
+        PackArgs a{h->d_count.p, h->d_kps.p, h->d_desc.p, h->d_uR.p, h->d_depth.p, h->d_status.p, h->geo.kp_cap,
+                   rec_bytes};
+        CompactScales sc{};
+        for (int l = 0; l < kMaxLevels; ++l) sc.inv_scale[l] = l < h->geo.nlevels ? h->geo.inv_scale[l] : 1.f;
+        if (h->batch_done_rec) HIPCK(hipStreamWaitEvent((hipStream_t)hip_stream, h->batch_done, 0));
+        HIPCK(launch_pack_compact(a, sc, d_records, pair0, n_pairs, (hipStream_t)hip_stream));
+    });
+}
+
 int orbfe_batch_fetch(orbfe_handle h, int32_t image, orbfe_keypoint* kps, uint8_t* desc, int32_t cap, int32_t* n_out) {
     return guarded([&] {
         if (!h || !n_out) throw Error(ORBFE_EINVAL, "null argument");

@@ -53,6 +53,12 @@ struct PackArgs {
 };
 
 hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s);
+// k_pack_compact: the compact record layout (orbfe_batch_pack_compact_device); inverse level scales by octave
+struct CompactScales {
+    float inv_scale[kMaxLevels];
+};
+hipError_t launch_pack_compact(const PackArgs& a, const CompactScales& sc, uint8_t* out, int pair0, int n_pairs,
+                               hipStream_t s);
 // k_copy_segments: up to 12 dword copies in one launch (dst may be device-visible page-locked host memory)
 struct CopySegs {
     struct Seg {

@@ -55,6 +55,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc(const void* p, ui
 
 // Wave-wide sum (wave-uniform result): DPP quad_perm / row_ror sums inside each 16-lane row, then the
 // four row sums through v_readlane (no LDS-crossbar round trips).
+// Two wave-wide sums at once: the DPP steps of the two interleave, so neither waits out the other's
+// VALU-write -> DPP-read hazard (the s_nop the compiler puts between dependent DPP adds).
+__device__ __forceinline__ void wave_sum2(int& a, int& b) {
+    a += __builtin_amdgcn_update_dpp(0, a, 0xB1, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0xB1, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x4E, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x4E, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x124, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x124, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x128, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x128, 0xF, 0xF, false);
+    a = __builtin_amdgcn_readlane(a, 0) + __builtin_amdgcn_readlane(a, 16) + __builtin_amdgcn_readlane(a, 32) +
+        __builtin_amdgcn_readlane(a, 48);
+    b = __builtin_amdgcn_readlane(b, 0) + __builtin_amdgcn_readlane(b, 16) + __builtin_amdgcn_readlane(b, 32) +
+        __builtin_amdgcn_readlane(b, 48);
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
@@ -2451,7 +2468,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             a01 = __builtin_amdgcn_udot4(m, (sl >> 9) * 0x01010101u, a01, false);  // row weight r = v + 15
             a1 = __builtin_amdgcn_udot4(m, 0x01010101u, a1, false);
         }
-        const int m10 = wave_sum((int)a10 - 18 * (int)a1), m01 = wave_sum((int)a01 - 15 * (int)a1);
+        int m10 = (int)a10 - 18 * (int)a1, m01 = (int)a01 - 15 * (int)a1;
+        wave_sum2(m10, m01);
         const float angle = fast_atan2_uniform(m01, m10);
         float b, a;
         glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
@@ -2595,10 +2613,12 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // [floor(y - 2s), ceil(y + 2s)] (double arithmetic, s = scale of its octave).  One workgroup per pair:
 // LDS histogram -> block scan -> fill.  The order inside a bucket is irrelevant: k_stereo reduces
 // (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
-// Also writes the compact (x, octave) record of every right keypoint.  1 024 threads: the kernel is one
-// latency chain per pair (load, count, scan, fill), so small batches (a frame's one pair) wait on it whole.
-constexpr int kBkThreads = 1024;
-__global__ __launch_bounds__(kBkThreads) void k_stereo_bucket(Geo g, StereoArgs A) {
+// Also writes the compact (x, octave) record of every right keypoint.  NT = 1 024 threads for small batches:
+// the kernel is one latency chain per pair (load, count, scan, fill), and a frame's one pair waits on it
+// whole; 256 for large ones, whose many workgroups share the CUs with the other streams' stages.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_stereo_bucket(Geo g, StereoArgs A) {
+    constexpr int kBkThreads = NT;
     extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
     __shared__ int scan_tmp[257];
     const int pr = blockIdx.x, t = threadIdx.x;
@@ -3186,7 +3206,10 @@ hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const u
 }
 
 hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
-    hipLaunchKernelGGL(k_stereo_bucket, dim3(n_pairs), dim3(kBkThreads), (size_t)4 * (g.H + 1), s, g, a);
+    if (2 * n_pairs < kSmallBatchImages)
+        hipLaunchKernelGGL(k_stereo_bucket<1024>, dim3(n_pairs), dim3(1024), (size_t)4 * (g.H + 1), s, g, a);
+    else
+        hipLaunchKernelGGL(k_stereo_bucket<256>, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);
     hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + 15) / 16, n_pairs), dim3(256), 0, s, g, a);
     return hipGetLastError();
 }
@@ -3226,6 +3249,51 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a, uint8_t* __restrict__ 
         while (o >= words[r]) o -= words[r++];
         ((uint32_t*)rec)[w] = src[r][o];
     }
+}
+
+// Compact records (orbfe_batch_pack_compact_device, pyorbslam_amd/dist.py unpack_compact): counts L, R (2 x i32)
+// | keypoints L, R (cap x {u32 x | y << 12 | octave << 24 in level pixels, f32 angle}) | descriptors L, R
+// (cap x 32 B) | u_right, depth (cap x f32) | scores L, R (cap x u8) | status (cap x i8): 8 + 91 cap bytes
+// against 8 + 121 cap.  A keypoint's x, y, size and response follow from (x, y, octave, score) on the host
+// exactly as k_orb computed them (x = f32(level x) * scale[octave]; the level coordinate is recovered here
+// as rint(x * inv_scale), exact for coordinates < 2^22).
+__global__ __launch_bounds__(256) void k_pack_compact(PackArgs a, CompactScales sc, uint8_t* __restrict__ out, int pair0) {
+    const int p = blockIdx.y, gp = pair0 + p, t = blockIdx.x * 256 + threadIdx.x, nt = gridDim.x * 256;
+    uint8_t* rec = out + (int64_t)p * a.rec_bytes;
+    const int64_t cap = a.kp_cap;
+    uint32_t* w = (uint32_t*)rec;
+    if (t < 2) w[t] = (uint32_t)a.count[2 * (int64_t)gp + t];
+    for (int s = 0; s < 2; ++s) {  // keypoints and scores of image 2 gp + s
+        const orbfe_keypoint* kp = a.kps + (2 * (int64_t)gp + s) * cap;
+        uint32_t* kw = w + 2 + s * 2 * cap;
+        uint8_t* sb = rec + 8 + cap * 88 + s * cap;
+        for (int64_t i = t; i < cap; i += nt) {
+            const orbfe_keypoint k = kp[i];
+            const int o = k.octave & 15;
+            const uint32_t x = (uint32_t)__float2int_rn(k.x * sc.inv_scale[o]) & 0xFFFu;
+            const uint32_t y = (uint32_t)__float2int_rn(k.y * sc.inv_scale[o]) & 0xFFFu;
+            kw[2 * i] = x | (y << 12) | ((uint32_t)o << 24);
+            kw[2 * i + 1] = __float_as_uint(k.angle);
+            sb[i] = (uint8_t)(int)k.response;
+        }
+    }
+    const uint32_t* d = (const uint32_t*)(a.desc + (2 * (int64_t)gp) * cap * 32);  // L then R: adjacent
+    uint32_t* dw = w + 2 + 4 * cap;
+    for (int64_t i = t; i < 16 * cap; i += nt) dw[i] = d[i];
+    uint32_t* uw = dw + 16 * cap;
+    for (int64_t i = t; i < cap; i += nt) {
+        uw[i] = __float_as_uint(a.u_right[gp * cap + i]);
+        uw[cap + i] = __float_as_uint(a.depth[gp * cap + i]);
+    }
+    uint8_t* st = rec + 8 + cap * 90;
+    for (int64_t i = t; i < cap; i += nt) st[i] = (uint8_t)a.status[gp * cap + i];
+}
+
+hipError_t launch_pack_compact(const PackArgs& a, const CompactScales& sc, uint8_t* out, int pair0, int n_pairs,
+                               hipStream_t s) {
+    if (n_pairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_compact, dim3(16, n_pairs), dim3(256), 0, s, a, sc, out, pair0);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, hipStream_t s) {

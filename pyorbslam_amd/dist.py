@@ -75,6 +75,42 @@ def unpack(kp_cap: int, rec: np.ndarray) -> dict:
 _GATHER_BUF: dict = {}
 
 
+def compact_record_bytes(kp_cap: int) -> int:
+    """orbfe_batch_pack_compact_device's record: 8 + 91 kp_cap bytes, padded to 16 (include/orbfe.h)."""
+    return (8 + 91 * kp_cap + 15) // 16 * 16
+
+
+def unpack_compact(kp_cap: int, rec: np.ndarray, scales) -> dict:
+    """A compact record back to unpack()'s arrays, bit for bit: x = f32(level x) * scale[octave], size =
+    (float)(int)(31 * scale[octave]) (ORBextractor.cpp:836, 1094-1099: what k_orb wrote), response = score;
+    scales: the extractor's float32 scale factors (orbfe_get_scales)."""
+    sc = np.asarray(scales, np.float32)
+    size = np.array([float(int(np.float32(31) * v)) for v in sc], np.float32)
+    nl, nr = rec[0:8].view(np.int32).tolist()
+    out = {}
+    o_kp, o_desc, o_st = 8, 8 + 16 * kp_cap, 8 + 80 * kp_cap
+    for s, (name, n) in enumerate((("kps_left", nl), ("kps_right", nr))):
+        kw = rec[o_kp + 8 * kp_cap * s:o_kp + 8 * kp_cap * s + 8 * n].view(np.uint32).reshape(n, 2)
+        xyo = kw[:, 0]
+        oct_ = (xyo >> 24).astype(np.int32)
+        k = np.empty(n, KP_DTYPE)
+        k["x"] = (xyo & 0xFFF).astype(np.float32) * sc[oct_]
+        k["y"] = ((xyo >> 12) & 0xFFF).astype(np.float32) * sc[oct_]
+        k["size"] = size[oct_]
+        k["angle"] = kw[:, 1].view(np.float32)
+        o_sc = 8 + 88 * kp_cap + s * kp_cap
+        k["response"] = rec[o_sc:o_sc + n].astype(np.float32)
+        k["octave"] = oct_
+        out[name] = k
+    for s, (name, n) in enumerate((("desc_left", nl), ("desc_right", nr))):
+        out[name] = rec[o_desc + 32 * kp_cap * s:o_desc + 32 * kp_cap * s + 32 * n].reshape(n, 32).copy()
+    out["u_right"] = rec[o_st:o_st + 4 * nl].view(np.float32).copy()
+    out["depth"] = rec[o_st + 4 * kp_cap:o_st + 4 * kp_cap + 4 * nl].view(np.float32).copy()
+    o = 8 + 90 * kp_cap
+    out["status"] = rec[o:o + nl].view(np.int8).copy()
+    return out
+
+
 def gather_buffer(world: int, records):
     """dst's receive buffer for gather_records: one (world * local_pairs, record_bytes) tensor per (shape,
     dtype, device), allocated on first use and reused by every later gather of that shape."""
@@ -130,33 +166,35 @@ def gather_results(records: np.ndarray, n_pairs_total: int, device=None, dst: in
     return np.concatenate([full[r, :shard(n_pairs_total, world, r)[1]] for r in range(world)], axis=0)
 
 
-def pack_device(frontends, counts, out) -> None:
-    """Pack every pair of the handles' last stereo batches into `out` ((sum(counts), record_bytes) uint8 device
-    tensor, handle-major) with k_pack on the current stream; orbfe_batch_pack_device orders each pack after
-    the batch that produced its results, whatever stream that batch ran on."""
+def pack_device(frontends, counts, out, compact: bool = False) -> None:
+    """Pack every pair of the handles' last stereo batches into `out` ((sum(counts), record bytes) uint8 device
+    tensor, handle-major) with k_pack (compact: k_pack_compact) on the current stream; the pack orders itself
+    after the batch that produced its results, whatever stream that batch ran on."""
     import ctypes as C
     import torch
     from ._lib import call
     rb = out.shape[1]
     st = torch.cuda.current_stream(out.device).cuda_stream
+    fn = "orbfe_batch_pack_compact_device" if compact else "orbfe_batch_pack_device"
     o = 0
     for f, n in zip(frontends, counts):
         if n:
-            call("orbfe_batch_pack_device", f.handle, C.c_void_p(out[o].data_ptr()), rb, 0, n, C.c_void_p(st))
+            call(fn, f.handle, C.c_void_p(out[o].data_ptr()), rb, 0, n, C.c_void_p(st))
         o += n
 
 
 def timed_gather(frontends, counts, device, world: int, rank: int, max_local: int | None = None,
-                 reps: int = 3) -> dict:
-    """Pack (k_pack) + gather to rank 0 of every pair's results, timed like the bench step (barrier +
-    synchronise on both sides, max over ranks); every rank sends max_local records (its own pairs, padded:
-    uneven shards of a strong-scaling run).  The records of rank 0's own first pair are checked against
-    orbfe_batch_fetch."""
+                 reps: int = 3, compact: bool = True) -> dict:
+    """Pack (k_pack_compact: compact records, 25 % fewer bytes over xGMI) + gather to rank 0 of every pair's
+    results, timed like the bench step (barrier + synchronise on both sides, max over ranks); every rank
+    sends max_local records (its own pairs, padded: uneven shards of a strong-scaling run).  The records of
+    rank 0's own first pair are checked against orbfe_batch_fetch."""
     import torch
     import torch.distributed as dist
     n_local = int(sum(counts))
     max_local = n_local if max_local is None else int(max_local)
-    rb = record_bytes(frontends[0].kp_cap)
+    kc = frontends[0].kp_cap
+    rb = compact_record_bytes(kc) if compact else record_bytes(kc)
     buf = torch.zeros((max_local, rb), dtype=torch.uint8, device=device)
     times = []
     full = None
@@ -165,7 +203,7 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
             dist.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        pack_device(frontends, counts, buf)
+        pack_device(frontends, counts, buf, compact)
         # RCCL gathers the device buffer in place; a gloo rehearsal (several ranks on one GPU) stages it
         full = gather_records(buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu(), 0)
         torch.cuda.synchronize(device)
@@ -179,14 +217,19 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
         dt = float(t.item())
     ok = None
     if rank == 0:
-        u = unpack(frontends[0].kp_cap, full[0].cpu().numpy())
+        rec0 = full[0].cpu().numpy()
+        u = unpack_compact(kc, rec0, frontends[0].scales) if compact else unpack(kc, rec0)
         k, d = frontends[0].fetch_image(0)
+        kr, dr = frontends[0].fetch_image(1)
         s = frontends[0].fetch_stereo(0)
         ok = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
-              and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["status"], s["status"]))
+              and u["kps_right"].tobytes() == kr.tobytes() and np.array_equal(u["desc_right"], dr)
+              and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["depth"], s["depth"])
+              and np.array_equal(u["status"], s["status"]))
         if not ok:
             raise RuntimeError("gathered record of pair 0 differs from orbfe_batch_fetch")
-    return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "pairs_gathered": world * max_local,
+    return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "records": "compact" if compact else "full",
+            "pairs_gathered": world * max_local,
             "bytes_to_rank0": world * max_local * rb, "record_check": ok,
             "GBs_into_rank0": round(world * max_local * rb / dt / 1e9, 2),
             "what": "k_pack on every rank + one gather of the records to rank 0 (RCCL with nccl, gloo on CPU), "

@@ -226,25 +226,34 @@ def test_pair_path_empty_image():
     assert len(a.stereo_result["status"]) == 0
 
 
-def test_device_pack_records_match_fetch():
-    """k_pack (orbfe_batch_pack_device) builds the gather records of dist.py on the device: every field of
-    every pair decodes to what orbfe_batch_fetch / _fetch_stereo return."""
+@pytest.mark.parametrize("compact", [False, True])
+def test_device_pack_records_match_fetch(compact):
+    """k_pack / k_pack_compact (orbfe_batch_pack_device / _compact_device) build the gather and host-fed
+    records of dist.py on the device: every field of every pair decodes (unpack / unpack_compact, which
+    rebuilds x, y, size and response from level coordinates, octave and score) to exactly what
+    orbfe_batch_fetch / _fetch_stereo return, for the KITTI and the EuRoC geometries."""
     torch = pytest.importorskip("torch")
     from pyorbslam_amd import dist as D
     from pyorbslam_amd.batch import StereoFrontEnd
-    imgs = torch.from_numpy(synth.make_batch(3, seed0=70)).cuda()
-    fes = [StereoFrontEnd(max_pairs=3, lanes=1), StereoFrontEnd(max_pairs=3, lanes=2)]
-    for f in fes:
-        f.enqueue(imgs, 3)
-    torch.cuda.synchronize()
-    rb = D.record_bytes(fes[0].kp_cap)
-    buf = torch.zeros((6, rb), dtype=torch.uint8, device="cuda")
-    D.pack_device(fes, [3, 3], buf)
-    torch.cuda.synchronize()
-    host = buf.cpu().numpy()
+    for w, h, nf in ((1241, 376, 2000), (752, 480, 1000)):
+        imgs = torch.from_numpy(synth.make_batch(3, seed0=70, width=w, height=h)).cuda()
+        fes = [StereoFrontEnd(w, h, max_pairs=3, nfeatures=nf, lanes=1), StereoFrontEnd(w, h, max_pairs=3, nfeatures=nf,
+                                                                                    lanes=2)]
+        for f in fes:
+            f.enqueue(imgs, 3)
+        torch.cuda.synchronize()
+        rb = (D.compact_record_bytes if compact else D.record_bytes)(fes[0].kp_cap)
+        buf = torch.zeros((6, rb), dtype=torch.uint8, device="cuda")
+        D.pack_device(fes, [3, 3], buf, compact)
+        torch.cuda.synchronize()
+        host = buf.cpu().numpy()
+        _check_records(fes, host, compact, D)
+
+
+def _check_records(fes, host, compact, D):
     for i, f in enumerate(fes):
         for p in range(3):
-            u = D.unpack(f.kp_cap, host[3 * i + p])
+            u = D.unpack_compact(f.kp_cap, host[3 * i + p], f.scales) if compact else D.unpack(f.kp_cap, host[3 * i + p])
             kl, dl = f.fetch_image(2 * p)
             kr, dr = f.fetch_image(2 * p + 1)
             s = f.fetch_stereo(p)
