@@ -506,7 +506,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
 // sample lies at (row, col) with row^2 + col^2 <= (18.385 + 0.708)^2 (the pattern's largest radius,
 // ORBextractor.cpp:150-408, plus rint's rounding), blurred row o = row + 18 reads H rows o .. o + 6 at column
 // col + 21.  Centroid slots: every dword of staged rows 6 .. 36 that holds a byte of the umax disc
-// (ORBextractor.cpp:77-104), with its byte mask, the m10 byte weights u + 18 and the m01 row weight.
+// (ORBextractor.cpp:77-104), with the signed byte weights u (m10) and v (m01) of its disc bytes (0 elsewhere).
 std::vector<uint32_t> orb_tables(const int* umax) {
     std::vector<uint32_t> t(kOrbTabWords, 0u);
     bool need[44][40] = {};
@@ -537,16 +537,18 @@ std::vector<uint32_t> orb_tables(const int* umax) {
         const int v = r - kHalfPatch, um = umax[v < 0 ? -v : v];
         for (int d = (17 - um) / 4; d <= (um + 17) / 4; ++d) {
             if (sl >= 256) throw Error(ORBFE_EINVAL, "k_orb: more than 256 centroid slots");
-            uint32_t mask = 0, wt = 0;
+            uint32_t wu = 0, wv = 0;  // signed byte weights u and v of the disc's bytes, 0 off the disc
             for (int b = 0; b < 4; ++b) {
                 const int u = 4 * d + b - 17;
-                if (u >= -um && u <= um) mask |= 0xFFu << (8 * b);
-                wt |= (uint32_t)(u + 18) << (8 * b);
+                if (u >= -um && u <= um) {
+                    wu |= (uint32_t)(uint8_t)(int8_t)u << (8 * b);
+                    wv |= (uint32_t)(uint8_t)(int8_t)v << (8 * b);
+                }
             }
-            cw[4 * sl] = mask;
-            cw[4 * sl + 1] = wt;
+            cw[4 * sl] = wu;
+            cw[4 * sl + 1] = wv;
             cw[4 * sl + 2] = (uint32_t)((6 + r) * 12 + 2 + d);
-            cw[4 * sl + 3] = (uint32_t)r * 0x01010101u;
+            cw[4 * sl + 3] = 0u;
             ++sl;
         }
     }

@@ -2152,15 +2152,40 @@ __device__ __forceinline__ float sc_cos_poly(double x2) {
     const double c = __fma_rn(x4, sc::c2, c1);
     return (float)__fma_rn(x6, c2, c);
 }
-__device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
-    const unsigned top = (__float_as_uint(y) >> 20) & 0x7ff;
+// n / d correctly rounded for 0 <= n <= d with d in [1, 2^24], or n = 0: the compiler's IEEE __fdiv_rn sequence
+// (reciprocal, one Newton step on it, the quotient, two residual corrections) without its range scaling
+// (v_div_scale, v_div_fixup), which leaves such operands unchanged
+__device__ __forceinline__ float div_rn_unit(float n, float d) {
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float r = __fmaf_rn(__fmaf_rn(-d, r0, 1.0f), r0, r0);
+    float q = __fmul_rn(n, r);
+    q = __fmaf_rn(__fmaf_rn(-d, q, n), r, q);
+    return __fmaf_rn(__fmaf_rn(-d, q, n), r, q);
+}
+
+// cv::fastAtan2 of integer moments y, x (|y|, |x| < 2^24: the float conversions are exact), per lane (k_orb
+// evaluates a keypoint pair at once: lanes 0..31 one keypoint, 32..63 the other).  The same IEEE float
+// operations in the same order as cv::fastAtan2 on the converted floats (plain IEEE float ops, no
+// contraction): (ax >= ay) == (|x| >= |y|), (x < 0) == (x_int < 0); its three branches are selects.
+__device__ __forceinline__ float fast_atan2_lanes(int yi, int xi) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const int axi = xi < 0 ? -xi : xi, ayi = yi < 0 ? -yi : yi;
+    const float num = (float)min(axi, ayi), den = (float)max(axi, ayi);  // xge: (ay, ax), else (ax, ay)
+    const float c = div_rn_unit(num, __fadd_rn(den, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
+    float a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    a = axi >= ayi ? a : __fsub_rn(90.f, a);
+    a = xi < 0 ? __fsub_rn(180.f, a) : a;
+    return yi < 0 ? __fsub_rn(360.f, a) : a;
+}
+// glibc sincosf for y in [0, 2 pi), per lane.  glibc evaluates the polynomials on y unreduced for y < 0.75
+// (top <= 0x3f3; below top 0x397 it returns (y, 1)); there the reduction gives n = 0 and x = y, and its
+// reduced branch returns the same two floats for every float in [0, 0.75) (checked exhaustively in double with
+// FMA: tools/dbg/sincos_paths.c), so only the reduced branch is issued and lanes never diverge.
+__device__ __forceinline__ void sincosf_glibc_lanes(float y, float* sn, float* cs) {
     double x = y;
-    if (top <= 0x3f3) {
-        const double x2 = x * x;
-        *sn = top <= 0x397 ? y : sc_sin_poly(x, x2);
-        *cs = top <= 0x397 ? 1.0f : sc_cos_poly(x2);
-        return;
-    }
     const double r = x * sc::hpi_inv;
     const int n = (((int)r) + 0x800000) >> 24;
     x = __fma_rn(-(double)n, sc::hpi, x);
@@ -2171,30 +2196,6 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* sn, float* cs) {
     *sn = (n & 1) ? cp : sp;
     *cs = (n & 1) ? sp : cp;
 }
-
-// cv::fastAtan2 of integer moments y, x (|y|, |x| < 2^24: the float conversions are exact), for
-// wave-uniform arguments: the branches are decided on the scalar unit from the integers, so only one
-// division and one polynomial are issued (a float comparison of converted values is a per-lane condition
-// to the compiler, which then issues both branches and selects).  The same IEEE float operations in the
-// same order as cv::fastAtan2 on the converted floats (plain IEEE float ops, no contraction):
-// (ax >= ay) == (|x| >= |y|), (x < 0) == (x_int < 0).
-__device__ __forceinline__ float fast_atan2_uniform(int yi, int xi) {
-    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
-    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
-    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
-    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
-    const int axi = xi < 0 ? -xi : xi, ayi = yi < 0 ? -yi : yi;
-    const bool xge = axi >= ayi;
-    const float num = (float)(xge ? ayi : axi), den = (float)(xge ? axi : ayi);
-    const float c = __fdiv_rn(num, __fadd_rn(den, (float)2.220446049250313e-16)), c2 = __fmul_rn(c, c);
-    float a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
-    if (!xge) a = __fsub_rn(90.f, a);
-    if (xi < 0) a = __fsub_rn(180.f, a);
-    if (yi < 0) a = __fsub_rn(360.f, a);
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(a)));
-}
-
-
 
 __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clamped for far-out rows
     p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
@@ -2207,14 +2208,15 @@ __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clam
 // (the pattern's largest radius) plus 0.71 px of rounding, so each keypoint needs the blur only on that
 // disc, i.e. the 7x7 taps of 43 x 43 unblurred pixels around it; the arithmetic is OpenCV's 8U fixed point
 // (SURVEY.md Appendix A.3): out = (sum_j k_j sum_i k_i I + 2^15) >> 16, k = [18,34,48,56,48,34,18].
-// One wavefront per keypoint, kOrbKpw consecutive keypoints of one level per wave (the next keypoint's
-// window loads are in flight while the current one is computed):
+// One wavefront per keypoint at a time, kOrbKpw consecutive keypoints of one level per wave, taken in pairs
+// that share one angle evaluation (lanes 0..31 / 32..63); the next window's loads are in flight while the
+// current one is computed:
 //  * staging: rows cy-21 .. cy+21, columns cx-25 .. cx+22 as 12 dwords per row in LDS (byte j = column
-//    cx - 25 + j, the same layout for every keypoint), re-aligned with v_alignbyte from one buffer
-//    dwordx4 + one dword load per third of a row; keypoints whose window reaches past the level (reflect-101
-//    at the w x h clone's border, as the reference blurs a clone of the level) load byte by byte;
+//    cx - 25 + j, the same layout for every keypoint), lane r re-aligning row r with v_alignbyte from three
+//    buffer dwordx4 + one dword loads; keypoints whose window reaches past the level (reflect-101 at the
+//    w x h clone's border, as the reference blurs a clone of the level) load byte by byte;
 //  * centroid on the staged unblurred bytes: the 213 dwords of the umax disc (rows 6 .. 36) from a table
-//    of (byte mask, m10 byte weights, dword, row weight), 3 v_dot4 each;
+//    of (signed byte weights u, v, dword), 2 signed v_dot4 each on the bytes I - 128;
 //  * horizontal taps: the 189 (row pair, 4-column group) items the disc needs (a per-lane table), 10 v_dot4
 //    with shifted byte weights per row, stored row-pair interleaved as u16 pairs (dword = (H[2m][c], H[2m+1][c]));
 //  * BRIEF: lane j evaluates bits j + 64 i (i = 0..3); each of its 8 samples takes its vertical taps from
@@ -2222,7 +2224,6 @@ __device__ __forceinline__ int reflect101c(int p, int n) {  // reflect-101, clam
 //    ballot per 64 bits.
 constexpr int kSrcRows = 43, kSrcDw = 12;
 constexpr int kHPairs = 22, kHGrp = 10, kHDw = 4 * kHGrp;  // H: 22 row pairs x 40 columns (dwords)
-constexpr int kStageItems = kSrcRows * 3;
 constexpr int kOrbHItems = 3;          // horizontal items per lane (189 of 192 used)
 constexpr int kOrbCSlots = 4;          // centroid slots per lane (213 of 256 used)
 
@@ -2243,7 +2244,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // tab: [0, 192) horizontal items (src dword | hbuf uint4 index << 16, ~0 = none), then 256 centroid slots
-// as uint4 (byte mask, m10 byte weights, src dword, row weight byte-broadcast) — built by the host
+// as uint4 (u byte weights, v byte weights, src dword, 0) — built by the host
 // (orbfe_host.hip: orb_tables).
 template <int WAVES, int kOrbKpw>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_orb(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
@@ -2252,7 +2253,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
                                                     const uint32_t* __restrict__ tab) {
     __shared__ float4 s_pat[256];
-    __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: (byte mask, m10 byte weights)
+    __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: signed byte weights (u, v)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
     __shared__ uint32_t s_h[WAVES][kHPairs * kHDw];       // horizontal taps, row-pair interleaved u16
     const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
@@ -2262,14 +2263,14 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wv = __builtin_amdgcn_readfirstlane(blk * WAVES + wid);
-    // the lane's centroid slots: window dword + row weight (two 16-bit halves per register), the same for
+    // the lane's centroid slots: window dword (two 16-bit halves per register), the same for
     // every keypoint
     const float4 pat_r = threadIdx.x < 256 ? ((const float4*)c_pattern)[threadIdx.x] : float4{};
     uint32_t cslot[kOrbCSlots / 2];
 #pragma unroll
     for (int k = 0; k < kOrbCSlots / 2; ++k) {
         const uint4 a = ((const uint4*)(tab + 192))[lane + 64 * (2 * k)], b = ((const uint4*)(tab + 192))[lane + 64 * (2 * k + 1)];
-        cslot[k] = (a.z | ((a.w & 0xFFu) << 9)) | ((b.z | ((b.w & 0xFFu) << 9)) << 16);
+        cslot[k] = a.z | (b.z << 16);  // window dwords; LDS byte addresses once the wave's window is known
     }
     uint2 cw_r[(64 * kOrbCSlots + 64 * WAVES - 1) / (64 * WAVES)];
 #pragma unroll
@@ -2322,6 +2323,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
 #pragma unroll
         for (int k = 0; k < kOrbHItems; ++k)
             hit[k] = (src_a + 4u * (hit[k] & 0xFFFFu)) | ((hb_a + 16u * (hit[k] >> 16)) << 16);
+#pragma unroll
+        for (int k = 0; k < kOrbCSlots / 2; ++k)
+            cslot[k] = (src_a + 4u * (cslot[k] & 0xFFFFu)) | ((src_a + 4u * (cslot[k] >> 16)) << 16);
     }
     if (threadIdx.x < 256) s_pat[threadIdx.x] = pat_r;
 #pragma unroll
@@ -2331,54 +2335,43 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     }
     __syncthreads();  // tables
     uint4 rw[3];
-    uint32_t rx[3], rsh = 0;
+    uint32_t rx, rsh = 0;
     auto key_of = [&](int j) { return (uint32_t)__builtin_amdgcn_readlane((int)mykey, j); };
     // columns cx - 25 .. cx + 22 inside the level: dword staging (rows past the top / bottom are reflected
-    // per item); otherwise byte loads with reflect-101 in both directions
+    // per lane); otherwise byte loads with reflect-101 in both directions
     auto inside = [&](int cx) { return cx >= 25 && cx + 22 < Lw; };
-    // the lane's staging item k: row it / 3, third it % 3 of the window (it = lane + 64 k)
-    // (row, third) offsets of the lane's items inside the window: constant per wave
-    int it_r[3];
-    uint32_t it_off[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int it = min(lane + 64 * k, kStageItems - 1), r = (it * 171) >> 9, t = it - 3 * r;  // it / 3 for it < 129
-        it_r[k] = r;
-        it_off[k] = (uint32_t)(r * stride + 16 * t);
-    }
-    auto row_off = [&](int k, int cy, bool rows_in) {  // byte offset from column cx - 25 of level row cy - 21
-        if (rows_in) return it_off[k];
-        const int y = reflect101c(cy - 21 + it_r[k], Lh);
-        return (uint32_t)((y - (cy - 21)) * stride) + (it_off[k] - (uint32_t)(it_r[k] * stride));
+    // lane r stages window row r (43 rows; lanes past them repeat the last row's loads and store nothing):
+    // three dwordx4 + one dword from the dword at or below the row's first byte
+    const int it_r = min(lane, kSrcRows - 1);
+    const uint32_t it_off = (uint32_t)(it_r * stride);
+    auto row_off = [&](int cy, bool rows_in) {  // byte offset from column cx - 25 of level row cy - 21
+        if (rows_in) return it_off;
+        const int y = reflect101c(cy - 21 + it_r, Lh);
+        return (uint32_t)((y - (cy - 21)) * stride);
     };
     auto issue = [&](int cx, int cy) {
         const bool rows_in = cy >= 21 && cy + 21 < Lh;
-        const uint32_t base = (uint32_t)((cy - 21) * stride + cx - 25) + bias;
-        rsh = 0;
+        const uint32_t a = (uint32_t)((cy - 21) * stride + cx - 25) + bias + row_off(cy, rows_in), al = a & ~3u;
+        rsh = a & 3u;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const uint32_t a = base + row_off(k, cy, rows_in), al = a & ~3u;
-            rsh |= (a & 3u) << (2 * k);
-            rw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, al, 0, 0));
-            rx[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 16u, 0, 0);
-        }
+        for (int k = 0; k < 3; ++k)
+            rw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, al + 16u * k, 0, 0));
+        rx = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 48u, 0, 0);
     };
-    auto commit = [&]() {  // re-align each item by its own start's misalignment (rsh, 2 bits per item)
+    auto commit = [&]() {  // re-align the row by its start's misalignment: window dwords 12 r .. 12 r + 11
+        if (lane < kSrcRows) {
+            const uint32_t w[13] = {rw[0].x, rw[0].y, rw[0].z, rw[0].w, rw[1].x, rw[1].y, rw[1].z,
+                                    rw[1].w, rw[2].x, rw[2].y, rw[2].z, rw[2].w, rx};
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int it = lane + 64 * k;
-            if (it < kStageItems) {
-                const uint32_t sh = (rsh >> (2 * k)) & 3u;
-                const uint32_t w[5] = {rw[k].x, rw[k].y, rw[k].z, rw[k].w, rx[k]};
-                *(uint4*)(src + 4 * it) =  // item it = row it / 3, third it % 3: dwords 4 it .. 4 it + 3
-                    uint4{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
-                          __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
-            }
+            for (int k = 0; k < 3; ++k)
+                *(uint4*)(src + 12 * lane + 4 * k) =
+                    uint4{__builtin_amdgcn_alignbyte(w[4 * k + 1], w[4 * k], rsh), __builtin_amdgcn_alignbyte(w[4 * k + 2], w[4 * k + 1], rsh),
+                          __builtin_amdgcn_alignbyte(w[4 * k + 3], w[4 * k + 2], rsh), __builtin_amdgcn_alignbyte(w[4 * k + 4], w[4 * k + 3], rsh)};
         }
     };
     auto stage_border = [&](int cx, int cy) {  // reflect-101 at the level border, byte by byte
         uint8_t* sb = (uint8_t*)src;
-        constexpr int NB = (kSrcRows * 4 * kSrcDw + 63) / 64, NR = 11;  // 33 bytes per lane, 11 loads in flight
+        constexpr int NB = (kSrcRows * 4 * kSrcDw + 63) / 64, NR = 8;  // 33 bytes per lane, 8 loads in flight
 #pragma unroll 1
         for (int j0 = 0; j0 < NB; j0 += NR) {
             uint32_t v[NR];
@@ -2409,23 +2402,22 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // keypoint j's descriptor, lane j its keypoint record.  A store inside the loop would sit in front of
     // the next window's loads in the in-order vmcnt, and the wait for those loads then waits for the store.
     uint32_t mine_lo = 0, mine_hi = 0, kp_x = 0, kp_y = 0, kp_angle = 0, kp_resp = 0;
-    for (int j = 0; j < nk; ++j) {
-        const uint32_t key = key_of(j);
-        const int score = (int)(key >> 24);
-        // ---- stage keypoint j: the previous keypoint's reads of src / hb are complete (waited before its
-        //      ballots, which precede this point)
+    // ---- stage the window whose loads are in flight (cx, cy): the wave's earlier reads of src / hb are
+    //      complete (each was waited before the ballot or the LDS store that consumed it)
+    auto stage = [&]() {
         wave_sync_lds();
         if (inside(cx)) commit();
         else stage_border(cx, cy);
         wave_sync_lds();
-        const int ccx = cx, ccy = cy;
-        if (j + 1 < nk) {  // next keypoint's loads in flight during this one's compute
-            const uint32_t k = key_of(j + 1);
-            cx = (int)(k & 0xFFF);
-            cy = (int)((k >> 12) & 0xFFF);
-            if (inside(cx)) issue(cx, cy);
-        }
-        // ---- horizontal taps of the disc's (row pair, group) items
+    };
+    auto prefetch = [&](int jn) {  // the loads of keypoint jn's window in flight from here
+        const uint32_t k = key_of(jn);
+        cx = (int)(k & 0xFFF);
+        cy = (int)((k >> 12) & 0xFFF);
+        if (inside(cx)) issue(cx, cy);
+    };
+    // ---- horizontal taps of the disc's (row pair, group) items: src -> hb
+    auto hpass = [&]() {
 #pragma unroll
         for (int k = 0; k < kOrbHItems; ++k) {
             {  // lanes without an item run the dummy one (orb_tables)
@@ -2457,35 +2449,37 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                     u32x4{pk(h[0][0], h[1][0]), pk(h[0][1], h[1][1]), pk(h[0][2], h[1][2]), pk(h[0][3], h[1][3])};
             }
         }
-        // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15)
-        uint32_t a10 = 0, a01 = 0, a1 = 0;
+    };
+    // ---- intensity centroid on the unblurred disc (rows 6 .. 36 = cy - 15 .. cy + 15) of the window in src,
+    //      on the bytes I - 128 (signed) with signed weights u, v (0 off the disc): the disc is symmetric,
+    //      so sum(u) = sum(v) = 0 over it and sum u (I - 128) = sum u I = m_10 (and m_01) exactly; per-lane
+    //      partial sums
+    auto centroid = [&](int& m10, int& m01) {
+        m10 = 0;
+        m01 = 0;
 #pragma unroll
         for (int k = 0; k < kOrbCSlots; ++k) {
-            const uint2 cw = s_cw[lane + 64 * k];  // unused slots: mask 0
-            const uint32_t sl = (cslot[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-            const uint32_t m = src[sl & 0x1FFu] & cw.x;
-            a10 = __builtin_amdgcn_udot4(m, cw.y, a10, false);
-            a01 = __builtin_amdgcn_udot4(m, (sl >> 9) * 0x01010101u, a01, false);  // row weight r = v + 15
-            a1 = __builtin_amdgcn_udot4(m, 0x01010101u, a1, false);
+            typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+            const uint2 cw = s_cw[lane + 64 * k];  // unused slots: weights 0
+            const uint32_t ad = (k & 1) ? cslot[k >> 1] >> 16 : cslot[k >> 1] & 0xFFFFu;
+            const int d = (int)(*(lds_c32*)(uintptr_t)ad ^ 0x80808080u);
+            m10 = __builtin_amdgcn_sdot4(d, (int)cw.x, m10, false);
+            m01 = __builtin_amdgcn_sdot4(d, (int)cw.y, m01, false);
         }
-        int m10 = (int)a10 - 18 * (int)a1, m01 = (int)a01 - 15 * (int)a1;
-        wave_sum2(m10, m01);
-        const float angle = fast_atan2_uniform(m01, m10);
-        float b, a;
-        glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &b, &a);
-        wave_sync_lds();  // hb complete
-        // ---- steered BRIEF with the vertical taps per sample: sample (row, col) is blurred row o = row + 18
-        //      (H rows o .. o + 6), column c = col + 21.  rint by the 1.5 * 2^23 trick: the f32 bits are
-        //      xb = 0x4B400000 + R with R = rint(row) in [-18, 18], so the row pair m = o >> 1 =
-        //      floor(R / 2) + 9 is (xb >> 1) - 0x25A00000, and the byte address of H pair (m, c) is one
-        //      v_mad_u32_u24 (which reads the low 24 bits of xb >> 1, 0xA00000 + floor(R / 2)) over one
-        //      v_lshl_add of the column bits; the constants fold into kc.  The 4 dwords P[m .. m + 3] hold
-        //      rows 2m .. 2m + 7: for even o the taps are their low / high halves in order, for odd o every
-        //      tap sits one u16 higher, so the data is shifted by 16 * (R & 1) bits (v_alignbit takes bits
-        //      4:0 of xb << 4) and the weights stay fixed.  The last dword's high half has weight 0.
-        typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-        const uint32_t kc = (uint32_t)(uintptr_t)(lds_u32*)hb + (uint32_t)(4 * (9 * kHDw + 21)) -
-                            (uint32_t)(4 * kHDw) * 0xA00000u - (__float_as_uint(12582912.0f) << 2);
+    };
+    // ---- steered BRIEF of keypoint jj from hb with the vertical taps per sample: sample (row, col) is
+    //      blurred row o = row + 18 (H rows o .. o + 6), column c = col + 21.  rint by the 1.5 * 2^23 trick:
+    //      the f32 bits are xb = 0x4B400000 + R with R = rint(row) in [-18, 18], so the row pair m = o >> 1 =
+    //      floor(R / 2) + 9 is (xb >> 1) - 0x25A00000, and the byte address of H pair (m, c) is one
+    //      v_mad_u32_u24 (which reads the low 24 bits of xb >> 1, 0xA00000 + floor(R / 2)) over one
+    //      v_lshl_add of the column bits; the constants fold into kc.  The 4 dwords P[m .. m + 3] hold
+    //      rows 2m .. 2m + 7: for even o the taps are their low / high halves in order, for odd o every
+    //      tap sits one u16 higher, so the data is shifted by 16 * (R & 1) bits (v_alignbit takes bits
+    //      4:0 of xb << 4) and the weights stay fixed.  The last dword's high half has weight 0.
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    const uint32_t kc = (uint32_t)(uintptr_t)(lds_u32*)hb + (uint32_t)(4 * (9 * kHDw + 21)) -
+                        (uint32_t)(4 * kHDw) * 0xA00000u - (__float_as_uint(12582912.0f) << 2);
+    auto brief = [&](float a, float b, int jj) {
 #pragma unroll 1
         for (int i = 0; i < 4; ++i) {
             const float4 pt = s_pat[lane + 64 * i];
@@ -2509,17 +2503,66 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3 >> (sh & 31u)), w2(18, 0), s, false);
                 v2[e] = s >> 16;
             }
-            const uint64_t bb = __ballot(v2[0] < v2[1]);
-            // lane 4 j + i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
+            const uint64_t bb = __ballot(v2[0] < v2[1]);  // one SDWA compare of the high halves
+            // lane 4 jj + i keeps this ballot: two v_writelane (a select chain or a store per iteration measured
             // 3-5 % slower in round 2)
-            mine_lo = writelane_m0(mine_lo, (uint32_t)bb, 4 * j + i);
-            mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), 4 * j + i);
+            mine_lo = writelane_m0(mine_lo, (uint32_t)bb, 4 * jj + i);
+            mine_hi = writelane_m0(mine_hi, (uint32_t)(bb >> 32), 4 * jj + i);
         }
-        if (lane == j) {
-            kp_x = __float_as_uint(l ? __fmul_rn((float)ccx, L.scale) : (float)ccx);
-            kp_y = __float_as_uint(l ? __fmul_rn((float)ccy, L.scale) : (float)ccy);
+    };
+    auto record = [&](int jj, int kx, int ky, float angle, uint32_t key) {
+        if (lane == jj) {
+            kp_x = __float_as_uint(l ? __fmul_rn((float)kx, L.scale) : (float)kx);
+            kp_y = __float_as_uint(l ? __fmul_rn((float)ky, L.scale) : (float)ky);
             kp_angle = __float_as_uint(angle);
-            kp_resp = __float_as_uint((float)score);
+            kp_resp = __float_as_uint((float)(int)(key >> 24));
+        }
+    };
+    // Keypoints in pairs (A = j, B = j + 1), so that one angle chain (fastAtan2 + sincosf, ~55 instructions
+    // that every lane would otherwise issue for one keypoint) serves two: lanes 0..31 evaluate A's, lanes
+    // 32..63 B's.  With one src and one hb buffer per wave the order is: stage A, H(A) -> hb, centroid A;
+    // stage B into src (A's src reads are done), centroid B; angles; BRIEF A; H(B) -> hb; BRIEF B.  The next
+    // window's loads are in flight from the previous stage on.
+    for (int j = 0; j < nk; j += 2) {
+        const bool has_b = j + 1 < nk;
+        const uint32_t keyA = key_of(j);
+        stage();
+        const int ax = cx, ay = cy;
+        if (has_b) prefetch(j + 1);
+        hpass();
+        int m10a, m01a, m10b = 0, m01b = 0;
+        centroid(m10a, m01a);
+        int bx = 0, by = 0;
+        uint32_t keyB = 0;
+        if (has_b) {
+            keyB = key_of(j + 1);
+            stage();
+            bx = cx;
+            by = cy;
+            if (j + 2 < nk) prefetch(j + 2);
+            centroid(m10b, m01b);
+        }
+        wave_sum2(m10a, m01a);
+        if (has_b) wave_sum2(m10b, m01b);
+        const bool lo = lane < 32;
+        const float ang = fast_atan2_lanes(lo ? m01a : m01b, lo ? m10a : m10b);
+        float sv, cv;
+        sincosf_glibc_lanes(__fmul_rn(ang, (float)(M_PI / 180.f)), &sv, &cv);
+        const float angA = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), 0));
+        const float aA = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 0));
+        const float bA = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 0));
+        const float angB = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), 32));
+        const float aB = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 32));
+        const float bB = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 32));
+        wave_sync_lds();  // hb complete
+        brief(aA, bA, j);
+        record(j, ax, ay, angA, keyA);
+        if (has_b) {
+            wave_sync_lds();  // BRIEF A's hb reads are complete (waited before its ballots)
+            hpass();
+            wave_sync_lds();  // hb complete
+            brief(aB, bB, j + 1);
+            record(j + 1, bx, by, angB, keyB);
         }
     }
     const int64_t o0 = (int64_t)img * g.kp_cap + pre[l] + k0;  // the wave's first output slot

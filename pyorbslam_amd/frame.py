@@ -251,7 +251,8 @@ def assign_features_to_grid(self) -> None:
     off = np.zeros(cols * rows + 1, np.int32)
     np.cumsum(np.bincount(cell, minlength=cols * rows), out=off[1:])
     fl, o = flat.tolist(), off.tolist()
-    self.mGrid = [[fl[o[ix * rows + iy]:o[ix * rows + iy + 1]] for iy in range(rows)] for ix in range(cols)]
+    cells = [fl[a:b] for a, b in zip(o, o[1:])]  # one new list per cell, column-major
+    self.mGrid = [cells[i:i + rows] for i in range(0, cols * rows, rows)]
     self._orbfe_grid = (id(self.mGrid), off, flat)
     self._orbfe_pts = (kps, pts)  # the keypoint coordinates as doubles, for the matcher's grid queries
 
