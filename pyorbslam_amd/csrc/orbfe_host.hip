@@ -439,7 +439,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         }
         Lg.ncell = (int)c.cells.size() - Lg.cell0;
         Lg.key_cap = key_cap;
-        key_off += key_cap;
+        key_off += (key_cap + 3) & ~3;  // 16-byte aligned levels (k_octree_bins reads its key cache as dwordx4)
         c.maxcell = std::max(c.maxcell, Lg.ncell);
         if (key_cap >= (1 << 24)) throw Error(ORBFE_EINVAL, "too many FAST candidates per level");
         // DistributeOctTree initial columns (:543-545)
@@ -486,7 +486,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.ws_bytes = std::max<int64_t>(ws, 256);
     g.shear_bytes = shear;
     g.slot_total = std::max<int64_t>(slot_off, 1);
-    g.key_total = std::max(key_off, 1);
+    g.key_total = std::max(key_off, 4);
     if (g.max_ncap >= 65535) throw Error(ORBFE_EINVAL, "nfeatures too large for the octree node index");
     // octree kernel: k_octree_bins unless its LDS carve exceeds 150 KiB (or the caller forces the
     // per-candidate k_octree, orbfe_set_octree_kernel); k_octree keeps the candidates in LDS when the node

@@ -1519,9 +1519,11 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
 //      in their old order);
 //   3. all waves give every key its final node (bin -> node map) and keep the first maximum response per
 //      node (response << 24 | 0xFFFFFF - key index, atomicMax); the list goes out in list order.
-// A division below depth D0 (never seen on KITTI / EuRoC / synthetic images, where the list ends at
-// depth <= 4; the host picks D0 with ~2 N bins) counts that node's children with an extra sweep of wave 0
-// over the keys of its bin.  Equal-size ties of the careful phase resolve by creation order, as in k_octree.
+// A division below depth D0 (the host picks D0 with ~2 N bins, at most 2 048: the synthetic batch images
+// end at depth <= 4, but the clustered corners of the C3 sequence's nearby planes reach depth 8 - 10 at
+// levels 0 / 1) counts that node's children with an extra sweep over the keys, which wave 0 hands to every
+// wave of the workgroup; the sweeps read the keys from a key-order copy the first sweep leaves in global
+// scratch.  Equal-size ties of the careful phase resolve by creation order, as in k_octree.
 constexpr int kObThreads = 256;
 #ifndef ORBFE_OB_BATCH
 #define ORBFE_OB_BATCH 8
@@ -1658,9 +1660,10 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                                                             const uint32_t* __restrict__ octab,
                                                             uint32_t* __restrict__ lvl_kp, int* __restrict__ lvl_count,
                                                             int* __restrict__ overflow, int maxcell,
+                                                            uint32_t* __restrict__ kcache_all,
                                                             long long* __restrict__ prof) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ int s_K, s_S, s_cur, s_nd;
+    __shared__ int s_K, s_S, s_cur, s_nd, s_cmd;
     const int img = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
     long long* pm = prof ? prof + ((int64_t)img * g.nlevels + l) * 64 : nullptr;
     auto mark = [&](int id) {
@@ -1744,9 +1747,6 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         const int y = min(max((int)((v >> 12) & 0xFFFu) - kBorder, 0), ny - 1);
         return X[x] | Y[y];
     };
-    // keys k = t, t + 256, ... (consecutive keys in consecutive lanes: coalesced slot reads and scratch
-    // writes; both sweeps use this mapping, so a thread reads back only what it wrote itself).  A key's
-    // cell by binary search over the cell offsets, kObBatch keys' searches and slot loads in flight.
     // Every key once: keys k = tid, tid + nthr, ... (consecutive keys in consecutive lanes: coalesced slot
     // reads), kObBatch of them in flight per thread; a key's cell is the cell of its 64-key block's first key
     // (bcell) walked forward over the few cells the block spans.  fn(k, slot value, code) for k < K.
@@ -1775,16 +1775,92 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             for (int u = 0; u < kObBatch; ++u) fn(k0 + nthr * u, v[u], key_code(v[u]));
         }
     };
+    // the first sweep also leaves every key's slot value in key order in global scratch (kc, the level's
+    // 16-byte aligned range of the handle's candidate scratch), so the later sweeps (children of nodes
+    // deeper than D0, the final map) read keys with dwordx4 loads instead of walking cells: for_cached,
+    // keys 4 (tid + nthr j) .. + 3, kObBatch / 2 loads in flight; fn(k, value, code) also for k >= K (the
+    // padding of the last 4 keys), which fn ignores.  Written and read inside this workgroup (same CU, the
+    // barrier between orders them).
+    uint32_t* kc = kcache_all + (int64_t)img * g.key_total + L.key_off;
+    auto for_cached = [&](int tid, int nthr, auto nbc, auto&& fn) {
+        constexpr int NB = decltype(nbc)::value;
+        for (int k0 = 4 * tid; k0 < K; k0 += 4 * nthr * NB) {
+            uint4 v[NB];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int k = k0 + 4 * nthr * u;
+                v[u] = k < K ? *(const uint4*)(kc + k) : uint4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int k = k0 + 4 * nthr * u;
+                fn(k, v[u].x, key_code(v[u].x));
+                fn(k + 1, v[u].y, key_code(v[u].y));
+                fn(k + 2, v[u].z, key_code(v[u].z));
+                fn(k + 3, v[u].w, key_code(v[u].w));
+            }
+        }
+    };
     mark(5);
     for_keys(t, NT, [&](int k, uint32_t v, uint32_t cd) {
         bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
+        if (k < K) kc[k] = v;
     });
     mark(6);
     __syncthreads();
     mark(1);
 
-    // ---- 2. wave 0: cumulative counts, initial columns (:543-584), the passes (:585-737)
-    if (t < 64) {
+    // The nn nodes deeper than D0 listed in d.dl (list `code`) sorted by code into d.sp (codes) / d.sd (list
+    // positions), by every thread (rank = number of smaller codes; the nodes are disjoint, so their
+    // left-aligned codes differ).  A key's node is then the last one whose code is <= the key's, if the
+    // key lies inside it: a binary search instead of a scan over all deep nodes per key.
+    auto deep_sort = [&](int nn, const uint32_t* code) {
+        for (int i = t; i < nn; i += NT) {
+            const int p = d.dl[i];
+            const uint32_t ci = code[p];
+            int r = 0;
+            for (int j = 0; j < nn; ++j) r += code[d.dl[j]] < ci;
+            d.sp[r] = (int)ci;
+            d.sd[r] = p;
+        }
+    };
+    // list position of the sorted deep node holding key code cd (-1: none)
+    auto deep_find = [&](int nn, const uint32_t* code, const uint8_t* dep, uint32_t cd) {
+        int lo = 0, hi = nn - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((uint32_t)d.sp[mid] <= cd) lo = mid; else hi = mid - 1;
+        }
+        const int p = d.sd[lo];
+        return (uint32_t)d.sp[lo] <= cd && ((cd ^ code[p]) >> (2 * (D - dep[p]))) == 0u ? p : -1;
+    };
+    // sweep over the keys for the children counts of the deep nodes (list `lst`): every wave takes part
+    // (wave 0 hands it out from inside its passes, see deep_counts)
+    auto deep_sweep = [&](int nn, int lst) {
+        const uint32_t* code = lst ? d.code1 : d.code0;
+        const uint8_t* dep = lst ? d.dep1 : d.dep0;
+        deep_sort(nn, code);
+        __syncthreads();
+        for_cached(t, NT, std::integral_constant<int, 1>{}, [&](int kk, uint32_t, uint32_t cd) {
+            if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
+            const int p = deep_find(nn, code, dep, cd);
+            if (p >= 0) {
+                const int q = (int)((cd >> (2 * (D - dep[p] - 1))) & 3u);
+                atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
+            }
+        });
+    };
+    // ---- 2. wave 0: cumulative counts, initial columns (:543-584), the passes (:585-737); the other waves
+    //      wait for deep sweeps (s_cmd: 1 | list << 1 with s_nd nodes; 0 when the passes are over)
+    if (t >= 64) {
+        for (;;) {
+            __syncthreads();  // a command (deep_counts) or the end of the passes
+            const int cmd = s_cmd;
+            if (cmd == 0) break;
+            deep_sweep(s_nd, cmd >> 1);
+            __syncthreads();  // sweep complete
+        }
+    } else {
         wave_scan_lds((int*)d.bins, B);
         if (t == 0) d.bins[B] = (uint32_t)K;
         wsync();
@@ -1850,21 +1926,13 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                 nd += __popcll(bm);
             }
             if (nd == 0) return;
-            wsync();
-            const uint32_t* code = L_code();
-            const uint8_t* dep = L_dep();
-            for_keys(t, 64, [&](int kk, uint32_t, uint32_t cd) {
-                if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
-                for (int i = 0; i < nd; ++i) {
-                    const int p = d.dl[i], dp = dep[p];
-                    if (((cd ^ code[p]) >> (2 * (D - dp))) == 0u) {
-                        const int q = (int)((cd >> (2 * (D - dp - 1))) & 3u);
-                        atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
-                        break;
-                    }
-                }
-            });
-            wsync();
+            if (t == 0) {
+                s_cmd = 1 | (cur << 1);
+                s_nd = nd;
+            }
+            __syncthreads();  // the other waves start the sweep
+            deep_sweep(nd, cur);
+            __syncthreads();  // every wave's counts are in
             for (int i = t; i < nd; i += 64) atomicAnd(&d.bins[L_code()[d.dl[i]] >> bsh], ~kObDeep);
             wsync();
         };
@@ -2071,8 +2139,10 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         if (t == 0) {
             s_S = S;
             s_cur = cur;
-            s_nd = nd;
+            s_cmd = 0;
         }
+        __syncthreads();  // the other waves leave their command loop
+        if (t == 0) s_nd = nd;  // (they have read s_nd for their last sweep before that barrier)
     }
     __syncthreads();
     mark(60);
@@ -2094,22 +2164,20 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         best[p] = m;
     }
     __syncthreads();
-    // nodes deeper than D0 (rare): a sweep over the keys of their bins (bin flag, then a prefix match)
+    // nodes deeper than D0: a sweep over the keys of their bins (bin flag, then the sorted deep nodes)
     if (nd > 0) {
         for (int i = t; i < nd; i += NT) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
         __syncthreads();
     }
-    if (nd > 0)
-        for_keys(t, NT, [&](int kk, uint32_t v, uint32_t cd) {
+    if (nd > 0) {
+        deep_sort(nd, code);
+        __syncthreads();
+        for_cached(t, NT, std::integral_constant<int, 2>{}, [&](int kk, uint32_t v, uint32_t cd) {
             if (kk >= K || d.bins[cd >> bsh] != kObDeep) return;
-            for (int i = 0; i < nd; ++i) {
-                const int q = d.dl[i];
-                if (((cd ^ code[q]) >> (2 * (D - dep[q]))) == 0u) {
-                    atomicMax(&best[q], (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)kk));
-                    break;
-                }
-            }
+            const int q = deep_find(nd, code, dep, cd);
+            if (q >= 0) atomicMax(&best[q], (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)kk));
         });
+    }
     __syncthreads();
     for (int p = t; p < S; p += NT) {
         const uint32_t bv = best[p];
@@ -3187,10 +3255,10 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
         const bool wide = variant == 2 || (variant != 1 && n_images < kSmallBatchImages);
         if (wide)
             hipLaunchKernelGGL(k_octree_bins<1024>, dim3(n_images, g.nlevels), dim3(1024), lds, s, g, cells, cell_count,
-                               slots, octab, lvl_kp, lvl_count, overflow, maxcell, prof);
+                               slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
         else
             hipLaunchKernelGGL(k_octree_bins<kObThreads>, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells,
-                               cell_count, slots, octab, lvl_kp, lvl_count, overflow, maxcell, prof);
+                               cell_count, slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
