@@ -32,7 +32,7 @@ import ctypes as C
 import operator
 import threading
 import weakref
-from itertools import repeat
+from itertools import compress, repeat
 
 import numpy as np
 
@@ -149,6 +149,12 @@ _UR_SET = frozenset((int, float, np.float32, np.float64))
 _DOUBLE_OR_INT_SET = frozenset((float, int, np.float64))
 _ANGLE = operator.attrgetter("angle")
 _OBSERVATIONS = operator.methodcaller("observations")
+_IN_VIEW = operator.attrgetter("mbTrackInView")
+_IS_BAD = operator.methodcaller("is_bad")
+_VIEW_COS = operator.attrgetter("mTrackViewCos")
+_TRACK_LEVEL = operator.attrgetter("mnTrackScaleLevel")
+_WORLD_POS = operator.methodcaller("get_world_pos")
+_DESCRIPTOR = operator.methodcaller("get_descriptor")
 
 
 def _frame_grid(frame):
@@ -380,26 +386,51 @@ class ORBMatcher:
         np.cumsum(cnt[rows], out=off2[1:])
         if len(rows) == 0:
             return rows, off2, np.zeros(0, np.int32)
-        qd = _descriptor_rows([pmps[r].get_descriptor() for r in rows.tolist()])
+        qd = _descriptor_rows(list(map(_DESCRIPTOR, map(pmps.__getitem__, rows.tolist()))))
         return rows, off2, np.ascontiguousarray(self._csr(qd, train, off2, idx), np.int32)
 
     # ORBMatcher.py:215-283
+    def _f_p_inputs(self, vp_map_points, th, b_factor):
+        """The searched map points of search_by_projection_f_p (tracked in view, then not bad: the reference's
+        two `continue`s in its order), their predicted levels and radii, with the per-point attribute reads
+        and calls as map() over C-level getters.  The radius is ORBMatcher's own radius_by_viewing_cos
+        evaluated over an array of doubles (`vc > 0.998` in double, then `r *= th`); None (run the reference
+        loop) when the method is overridden, a view cosine is not a double (a float32 one compares in float32)
+        or th is not a Python number."""
+        if type(self).radius_by_viewing_cos is not ORBMatcher.radius_by_viewing_cos:
+            return None
+        if b_factor and type(th) not in (int, float):
+            return None
+        cand = list(compress(vp_map_points, map(_IN_VIEW, vp_map_points)))
+        pmps = list(compress(cand, map(operator.not_, map(_IS_BAD, cand))))
+        vc = _f64_array(list(map(_VIEW_COS, pmps)))
+        if vc is None:
+            return None
+        r = np.where(vc > 0.998, 2.5, 4.0)
+        if b_factor:
+            r = r * th
+        return pmps, list(map(_TRACK_LEVEL, pmps)), r.tolist()
+
     def search_by_projection_f_p(self, frame, vp_map_points, th):
         n_matches = 0
         b_factor = th != 1.0
         radius = self.radius_by_viewing_cos
-        pmps, lvls, rads = [], [], []
-        for pMP in vp_map_points:
-            if not pMP.mbTrackInView:
-                continue
-            if pMP.is_bad():
-                continue
-            r = radius(pMP.mTrackViewCos)
-            if b_factor:
-                r *= th
-            pmps.append(pMP)
-            lvls.append(pMP.mnTrackScaleLevel)
-            rads.append(r)
+        pre = self._f_p_inputs(vp_map_points, th, b_factor) if isinstance(vp_map_points, (list, tuple)) else None
+        if pre is not None:
+            pmps, lvls, rads = pre
+        else:
+            pmps, lvls, rads = [], [], []
+            for pMP in vp_map_points:
+                if not pMP.mbTrackInView:
+                    continue
+                if pMP.is_bad():
+                    continue
+                r = radius(pMP.mTrackViewCos)
+                if b_factor:
+                    r *= th
+                pmps.append(pMP)
+                lvls.append(pMP.mnTrackScaleLevel)
+                rads.append(r)
         done = self._f_p_native(frame, pmps, lvls, rads)
         if done is not None:
             return done
@@ -459,7 +490,7 @@ class ORBMatcher:
             cand = [i for i, m, o in zip(range(n_last), lmps, lout) if m and not o]
         else:  # the reference's indexing (and its IndexError)
             cand = [i for i in range(n_last) if lmps[i] and not lout[i]]
-        pos = [lmps[i].get_world_pos() for i in cand]
+        pos = list(map(_WORLD_POS, map(lmps.__getitem__, cand)))
         proj = []
         if (pos and set(map(type, pos)) == _NDARRAY_SET and set(map(_SHAPE, pos)) == {(3, 1)}
                 and len(set(map(_DTYPE, pos))) == 1):

@@ -88,19 +88,28 @@ class ORBextractor:
                 raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
             return [a.copy() for a in self._pyr_cache]
         out = []
+        if self._pyr_src is not None and sheared:  # the frame path: every level out of one allocation
+            owner, side = self._pyr_src
+            shapes = []
+            for l in range(self._nlevels):
+                w, h = C.c_int32(), C.c_int32()
+                call("orbfe_frame_pyramid", owner.handle, side, l, None, C.byref(w), C.byref(h))
+                shapes.append((h.value, w.value))
+            buf = np.empty(sum(hh * ww for hh, ww in shapes), np.uint8)
+            o = 0
+            for l, (hh, ww) in enumerate(shapes):
+                a = buf[o:o + hh * ww].reshape(hh, ww)
+                o += hh * ww
+                call("orbfe_frame_pyramid", owner.handle, side, l, ptr(a), None, None)
+                out.append(a)
+            return out
+        if self._pyr_src is not None:
+            raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
         for l in range(self._nlevels):
             w, h = C.c_int32(), C.c_int32()
-            if self._pyr_src is not None and sheared:
-                owner, side = self._pyr_src
-                call("orbfe_frame_pyramid", owner.handle, side, l, None, C.byref(w), C.byref(h))
-                a = np.empty((h.value, w.value), np.uint8)
-                call("orbfe_frame_pyramid", owner.handle, side, l, ptr(a), C.byref(w), C.byref(h))
-            else:
-                if self._pyr_src is not None:
-                    raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
-                call("orbfe_pyramid", self._h, l, None, int(sheared), C.byref(w), C.byref(h))
-                a = np.empty((h.value, w.value), np.uint8)
-                call("orbfe_pyramid", self._h, l, ptr(a), int(sheared), C.byref(w), C.byref(h))
+            call("orbfe_pyramid", self._h, l, None, int(sheared), C.byref(w), C.byref(h))
+            a = np.empty((h.value, w.value), np.uint8)
+            call("orbfe_pyramid", self._h, l, ptr(a), int(sheared), C.byref(w), C.byref(h))
             out.append(a)
         return out
 
@@ -120,12 +129,17 @@ class ORBextractor:
         else:
             self._kps, self._desc = kps[:n].copy(), desc[:n].copy()
 
-    def _release_frame(self) -> None:
+    def _release_frame(self, replaced=None) -> None:
         """Before this handle's frame is replaced: the extractors still reading their pyramid from it get a
-        host copy of it (the right extractor of an earlier pair must keep its own pyramid)."""
+        host copy of it (the right extractor of an earlier pair must keep its own pyramid), except
+        `replaced`, the right extractor of the pair about to be extracted, whose results the new frame
+        replaces anyway (until then it reports no extraction, as after a failed call)."""
         for ex in self._dependents:
             if ex._pyr_src is not None and ex._pyr_src[0] is self:
-                ex._pyr_cache = ex.GetImagePyramid() if ex._extracted else None
+                if ex is replaced:
+                    ex._extracted = False
+                else:
+                    ex._pyr_cache = ex.GetImagePyramid() if ex._extracted else None
                 ex._pyr_src = None
         self._dependents = []
 
@@ -164,7 +178,7 @@ class ORBextractor:
         if L.shape != R.shape:
             raise RuntimeError("left and right images differ in size")
         h, w = L.shape
-        self._release_frame()
+        self._release_frame(replaced=right_extractor)
         call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
              int(bool(want_pyramid)))
         cap = self._cap()
