@@ -582,8 +582,10 @@ def roofline_block(stage_ms: dict, P: int, width: int, height: int, nfeatures: i
             "pipeline_frac": (round(sum(inst.values()) * pairs_per_s_per_gpu / P / 1e9 / VALU_PEAK_GIPS, 4)
                               if pairs_per_s_per_gpu else None),
             "source": vi_src + " (rocprofv3 --pmc SQ_INSTS_VALU)"}
-        if "busy" in vi:  # per-stage VALU-busy fraction from SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES (tools/valu.py)
-            out["valu_roofline"]["busy"] = vi["busy"]
+        if "busy" in vi:  # per-stage VALU-busy fraction from the busy-cycle pass (tools/valu.py)
+            out["valu_roofline"]["valu_busy"] = {s: b.get("valu_busy") for s, b in vi["busy"].items()}
+            out["valu_roofline"]["valu_busy_def"] = ("4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): "
+                                                     "share of SIMD cycles issuing VALU, same standalone pass")
     else:
         out["valu_roofline"] = {"dropped": vi_src}
     return out

@@ -2,7 +2,7 @@
 # GPU evidence for one revision: parity tests, the default bench line (throughput + its own parity sample +
 # C4 / C4 rank share / C5 EuRoC / host-fed / C3 / standalone per-stage roofline / cpu_baseline), the C3
 # frame-mode line, the launcher refusal and a 2-rank gloo run, rocprofv3 kernel traces (default bench, the
-# 8-pair share, the frame path), and the PMC passes (one counter group per pass, MI355X_MICROARCH.md) over the
+# 8-pair share, the frame path, the C3 replay's frames), and the PMC passes (one counter group per pass, MI355X_MICROARCH.md) over the
 # standalone pass (--roofline-only) for KITTI and EuRoC: FETCH_SIZE, WRITE_SIZE (profiles/traffic.json via
 # tools/traffic.py), SQ_INSTS_VALU + SQ_INSTS_LDS + GRBM_GUI_ACTIVE, and the busy-cycle group
 # SQ_ACTIVE_INST_VALU + SQ_BUSY_CYCLES + SQ_WAIT_INST_ANY + GRBM_GUI_ACTIVE (profiles/valu.json via tools/valu.py).
@@ -34,6 +34,7 @@ step bench_gpus2_gloo 300 env ORBFE_DIST_BACKEND=gloo python bench.py --gpus 2 -
 step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ktrace" -o run -- python bench.py --cpu-sample 0 --no-c4 --no-host-fed --no-c3 --no-c5
 step ktrace_share8 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_share8" -o run -- python tools/small_trace.py --pairs 8 --steps 50
 step ktrace_frame 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_frame" -o run -- python tools/small_trace.py --frame --steps 50
+step ktrace_c3 200 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_c3" -o run -- python bench.py --mode frame --steps 96 --warmup 1
 for cam in kitti euroc; do
   args="--roofline-only --roofline-steps 2"
   [ $cam = euroc ] && args="$args --width 752 --height 480 --nfeatures 1000"
