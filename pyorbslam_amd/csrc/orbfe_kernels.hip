@@ -394,7 +394,11 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         const int dx = 4 * grp;
         const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
         const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-        auto row = [&](int rr) {
+        // psy / hp: the previous row's second source row and its taps (full waves walk consecutive rows, and a
+        // row's first source row is mostly the previous row's second: its taps are reused, not recomputed)
+        int psy = -1;
+        uint32_t hp[4] = {0u, 0u, 0u, 0u};
+        auto row = [&](int rr, bool reuse) {
             const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
             const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
             const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
@@ -413,8 +417,18 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
                                               __builtin_bit_cast(us2, aa.w), 0u, false);
             };
             uint32_t h0[4], h1[4];
-            taps(r0, h0);
+            if (reuse && y.sy0 == psy) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h0[k] = hp[k];
+            } else {
+                taps(r0, h0);
+            }
             taps(r1, h1);
+            if (reuse) {
+                psy = y.sy1;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hp[k] = h1[k];
+            }
             uint32_t v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
@@ -427,10 +441,12 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
                                                   (uint32_t)(rr * L.pitch), 0);
         };
-        if (!remwave) {
-            for (int rr = set; rr < nrow; rr += nset) row(rr);
+        if (!remwave) {  // set s: rows [s * per, (s + 1) * per), consecutive
+            const int per = (nrow + nset - 1) / nset, rend = min(set * per + per, nrow);
+            psy = -1;
+            for (int rr = set * per; rr < rend; ++rr) row(rr, true);
         } else {
-            for (int rr = row0; rr < nrow; rr += rstep) row(rr);
+            for (int rr = row0; rr < nrow; rr += rstep) row(rr, false);
         }
         if (!MULTI) return;  // one chunk per wave (every level up to 2 048 px): round 3's code exactly
         ch += ch_step;
