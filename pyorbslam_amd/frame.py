@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import sys
+from itertools import starmap
 
 import numpy as np
 
@@ -97,7 +98,7 @@ def extract_orb(self, flag, image) -> None:
             self.mvKeys_, self.mDescriptors = keypoint_tuples(kl), dl
         else:
             self.mvKeys_, self.mDescriptors = left.operator_kd(image)
-        self.mvKeys = [KeyPoint(*kp) for kp in self.mvKeys_]
+        self.mvKeys = list(starmap(KeyPoint, self.mvKeys_))  # [KeyPoint(*kp) for kp in mvKeys_], Frame.py:117
         if isinstance(left, ORBextractor) and len(left.last_keypoints) == len(self.mvKeys):
             # the keypoints' pt as doubles straight from the extractor's float32 fields (the values the
             # KeyPoints were built from), for assign_features_to_grid while mvKeys is still this list
@@ -109,7 +110,7 @@ def extract_orb(self, flag, image) -> None:
             self.mvKeysRight_, self.mDescriptorsRight = keypoint_tuples(pend[0]), pend[1]
         else:
             self.mvKeysRight_, self.mDescriptorsRight = right.operator_kd(image)
-        self.mvKeysRight = [KeyPoint(*kp) for kp in self.mvKeysRight_]
+        self.mvKeysRight = list(starmap(KeyPoint, self.mvKeysRight_))  # Frame.py:121
 
 
 # Frame.__init__'s attributes that come straight from its arguments (Frame.py:15-44), which Frame.copy

@@ -257,3 +257,25 @@ def test_resize_cascade_equals_per_level_launches(shape, params):
         call("orbfe_microbench", ex.handle, 0, 100 + S, 1, C.byref(ms))
         for l, (g, o) in enumerate(zip(ex.GetImagePyramid(sheared=False), orc.pyramid())):
             assert np.array_equal(g, o), f"cascade S={S} level {l}"
+
+
+def test_deep_octree_nodes_batch_and_single():
+    """Frames 60-75 of the C3 sequence cluster their level-0 / level-1 corners so that the octree divides
+    hundreds of nodes below the bin depth D0 (tools/octree_profile.py --seq; DESIGN §4 k_octree_bins, round
+    4): the all-wave deep sweeps over the cached keys, in the 256-thread batch variant (32 images) and the
+    1 024-thread one (one image), against the oracle on a sample of the images."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd.batch import StereoFrontEnd
+    seq = synth.StereoSequence(0, 1241, 376, 0.6)
+    imgs = np.stack([im for k in range(60, 76) for im in seq.frame(k)])
+    fe = StereoFrontEnd(max_pairs=16, lanes=1)
+    fe.enqueue(torch.from_numpy(imgs).cuda(), 16)
+    assert fe.overflow() == 0
+    ex = ORBextractor(**KITTI)
+    ox = O.OracleExtractor(**KITTI)
+    for i in (0, 9, 19, 30):
+        okps, odesc = ox.extract(imgs[i])
+        kps, desc = fe.fetch_image(i)
+        assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc), f"batch image {i}"
+        k1, d1 = ex.extract(imgs[i])
+        assert k1.tobytes() == okps.tobytes() and np.array_equal(d1, odesc), f"single image {i}"

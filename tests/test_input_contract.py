@@ -50,3 +50,18 @@ def test_dims_and_channels():
     with pytest.raises(RuntimeError, match="multi-channel"):
         as_gray_u8(np.zeros((40, 40, 3), np.uint8))
     assert as_gray_u8(np.zeros((40, 40, 1), np.uint8)).shape == (40, 40)
+
+
+def test_keypoint_tuples_equal_structured_tolist():
+    """keypoint_tuples builds the caster's tuples from per-field lists: the same values and element types as
+    the structured array's tolist (Python floats, an int octave)."""
+    from pyorbslam_amd._lib import KP_DTYPE
+    from pyorbslam_amd.pyORBExtractor import keypoint_tuples
+    rng = np.random.default_rng(0)
+    a = np.zeros(257, KP_DTYPE)
+    for f in ("x", "y", "size", "angle", "response"):
+        a[f] = rng.random(257).astype(np.float32) * 1000
+    a["octave"] = rng.integers(0, 8, 257)
+    got, ref = keypoint_tuples(a), a.tolist()
+    assert got == ref and [tuple(map(type, t)) for t in got] == [tuple(map(type, t)) for t in ref]
+    assert keypoint_tuples(a[:0]) == []

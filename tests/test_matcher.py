@@ -327,3 +327,51 @@ def test_fp_python_float_xr_takes_the_float32_path(case, monkeypatch):
     monkeypatch.setattr(matcher.ORBMatcher, "_f_p_native", lambda self, *a: None)
     assert matcher.ORBMatcher(0.8, True).search_by_projection_f_p(fr2, mps2, th2) == n_native
     assert np.array_equal(MF.encode_fp(fr2, mps2), got)
+
+
+def test_fp_inputs_equal_the_reference_loop():
+    """search_by_projection_f_p's vectorised prologue (_f_p_inputs) keeps the reference loop's map points
+    (tracked in view, then not bad), levels and radii (ORBMatcher.py:224-232, `r *= th` when th != 1), and
+    declines (None) where the loop must run: a float32 view cosine (compares in float32), an overridden
+    radius_by_viewing_cos, a numpy th."""
+    from pyorbslam_amd.matcher import ORBMatcher
+
+    class MP:
+        def __init__(self, inview, bad, vcos, lvl):
+            self.mbTrackInView, self._bad, self.mTrackViewCos, self.mnTrackScaleLevel = inview, bad, vcos, lvl
+
+        def is_bad(self):
+            return self._bad
+
+    rng = np.random.default_rng(3)
+    kinds = [float, np.float64, lambda v: np.array([v], np.float64)]
+    mps = [MP(bool(rng.random() < 0.8), bool(rng.random() < 0.1),
+              kinds[i % 3](float(rng.choice([0.998, 0.9980001, 0.5, 0.9999, 1.0]))), int(rng.integers(0, 8)))
+           for i in range(300)]
+
+    def loop(m, th):
+        out = ([], [], [])
+        for p in mps:
+            if not p.mbTrackInView or p.is_bad():
+                continue
+            r = m.radius_by_viewing_cos(p.mTrackViewCos)
+            if th != 1.0:
+                r *= th
+            out[0].append(p), out[1].append(p.mnTrackScaleLevel), out[2].append(r)
+        return out
+
+    m = ORBMatcher(0.8, True)
+    for th in (1, 1.0, 3, 2.5):
+        got = m._f_p_inputs(mps, th, th != 1.0)
+        ref = loop(m, th)
+        assert got[0] == ref[0] and got[1] == ref[1]
+        assert got[2] == ref[2] and all(type(v) is float for v in got[2])
+    assert m._f_p_inputs(mps, np.float32(2.0), True) is None
+    mps[0].mbTrackInView, mps[0]._bad, mps[0].mTrackViewCos = True, False, np.float32(0.998)
+    assert m._f_p_inputs(mps, 1, False) is None
+
+    class M2(ORBMatcher):
+        def radius_by_viewing_cos(self, view_cos):
+            return 3.0
+
+    assert M2(0.8, True)._f_p_inputs(mps, 1, False) is None

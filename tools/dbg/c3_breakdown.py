@@ -42,7 +42,7 @@ def _timed_call(name, *a):
 
 PX.call = _timed_call
 _rel = PX.ORBextractor._release_frame
-PX.ORBextractor._release_frame = lambda self: timed("release", _rel, self)
+PX.ORBextractor._release_frame = lambda self, **k: timed("release", _rel, self, **k)
 
 
 class Cached:
