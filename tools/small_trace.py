@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--graphs", type=int, default=1)
     ap.add_argument("--frame", action="store_true")
+    ap.add_argument("--pyramid", type=int, default=0, help="--frame: want_pyramid (the sheared views too)")
     a = ap.parse_args()
     import torch
     from pyorbslam_amd import synth
@@ -30,7 +31,7 @@ def main():
         call("orbfe_set_graphs", ex.handle, a.graphs)
         for k in range(5 + a.steps):
             call("orbfe_frame_extract", ex.handle, L.ctypes.data, R.ctypes.data, 1241, 376, 1241, KITTI_BF,
-                 float(np.float32(KITTI_FX)), 0)
+                 float(np.float32(KITTI_FX)), a.pyramid)
         return
     imgs = torch.from_numpy(synth.make_batch(a.pairs, seed0=0)).cuda()
     fe = StereoFrontEnd(max_pairs=a.pairs, lanes=1, graphs=bool(a.graphs))
