@@ -3435,16 +3435,26 @@ hipError_t launch_pack(const PackArgs& a, uint8_t* out, int pair0, int n_pairs, 
 // Several dword-aligned device -> (device-visible page-locked host) copies in one launch: the per-frame path's
 // results go to the host as one kernel's stores over PCIe instead of eight copy-engine transfers of a few
 // microseconds of fixed cost each.  blockIdx.y = segment.
+// 16-byte stores (the segments start 16-byte aligned: device allocations and 256-byte aligned offsets into the
+// page-locked buffer), the last dwords of a segment by block 0
 __global__ __launch_bounds__(256) void k_copy_segments(CopySegs a) {
     const CopySegs::Seg sg = a.seg[blockIdx.y];
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < sg.dwords; i += gridDim.x * 256u) sg.dst[i] = sg.src[i];
+    const uint32_t n4 = sg.dwords >> 2;
+    const uint4* src4 = (const uint4*)sg.src;
+    uint4* dst4 = (uint4*)sg.dst;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n4; i += gridDim.x * 256u) dst4[i] = src4[i];
+    if (blockIdx.x == 0 && threadIdx.x < (sg.dwords & 3u)) sg.dst[4 * n4 + threadIdx.x] = sg.src[4 * n4 + threadIdx.x];
 }
 
 hipError_t launch_copy_segments(const CopySegs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
     uint32_t most = 0;
-    for (int k = 0; k < a.n; ++k) most = std::max(most, a.seg[k].dwords);
-    const unsigned bx = std::max(1u, std::min((most + 1023u) / 1024u, 32u));
+    for (int k = 0; k < a.n; ++k) {
+        if (((uintptr_t)a.seg[k].src | (uintptr_t)a.seg[k].dst) & 15u) return hipErrorInvalidValue;
+        most = std::max(most, a.seg[k].dwords);
+    }
+    // enough waves for the PCIe stores of the largest segment (the frame's sheared views, ~0.7 M dwords)
+    const unsigned bx = std::max(1u, std::min((most / 4u + 1023u) / 1024u, 128u));
     hipLaunchKernelGGL(k_copy_segments, dim3(bx, a.n), dim3(256), 0, s, a);
     return hipGetLastError();
 }
