@@ -12,7 +12,15 @@ LIB := pyorbslam_amd/_lib/liborbfe.so
 OBJ := $(patsubst pyorbslam_amd/csrc/%.hip,pyorbslam_amd/_lib/%.o,$(SRC)) \
        $(patsubst pyorbslam_amd/csrc/%.cpp,pyorbslam_amd/_lib/%.o,$(CSRC))
 
-all: $(LIB) oracle
+# host-side CPython extension (no device code): the per-frame Python objects of the reference data model
+PY := python3
+PYHOST := pyorbslam_amd/_pyhost$(shell $(PY) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYINC := $(shell $(PY) -c "import sysconfig, numpy; print('-I' + sysconfig.get_paths()['include'], '-I' + numpy.get_include())")
+
+all: $(LIB) $(PYHOST) oracle
+
+$(PYHOST): pyorbslam_amd/csrc/orbfe_pyhost.cpp
+	g++ -O2 -std=c++17 -fPIC -shared -Wall $(PYINC) -o $@ $<
 
 pyorbslam_amd/_lib/%.o: pyorbslam_amd/csrc/%.hip $(HDR)
 	@mkdir -p pyorbslam_amd/_lib
@@ -36,7 +44,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf pyorbslam_amd/_lib
+	rm -rf pyorbslam_amd/_lib $(PYHOST)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

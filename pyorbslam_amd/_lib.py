@@ -145,6 +145,23 @@ def lib() -> C.CDLL:
     return _lib
 
 
+_pyhost = None
+
+
+def pyhost():
+    """The host-side CPython extension `_pyhost` (csrc/orbfe_pyhost.cpp): the per-frame Python objects of the
+    reference data model (KeyPoint tuples, Frame.mGrid, mvuRight / mvDepth) built in C.  Raises ImportError
+    when it is not built (`make`)."""
+    global _pyhost
+    if _pyhost is None:
+        try:
+            from . import _pyhost as m
+        except ImportError as e:
+            raise ImportError("pyorbslam_amd/_pyhost extension not built: run `make` (or __graft_entry__.build())") from e
+        _pyhost = m
+    return _pyhost
+
+
 def check(fn: str, rc: int) -> None:
     if rc != ORBFE_OK:
         raise OrbfeError(fn, rc, lib().orbfe_last_error().decode(errors="replace"))

@@ -21,7 +21,7 @@ from itertools import starmap
 
 import numpy as np
 
-from ._lib import call, ptr
+from ._lib import call, ptr, pyhost
 from .pyORBExtractor import ORBextractor, keypoint_tuples
 
 
@@ -39,6 +39,8 @@ def stereo_match_arrays(left: ORBextractor, right: ORBextractor, mbf: float, fx3
 
 def to_reference_lists(res: dict, kps_left: np.ndarray, mbf: float) -> tuple[list, list]:
     st = res["status"]
+    if type(mbf) is float:  # built in C (_pyhost.stereo_lists): the same element types as below
+        return pyhost().stereo_lists(res["u_right"], res["depth"], st, np.ascontiguousarray(kps_left["x"]), mbf)
     uR = list(res["u_right"])  # np.float32 scalars, as the reference's NumPy-2 float32 chain leaves them
     dep = list(res["depth"])
     for i in np.flatnonzero(st == 0).tolist():
@@ -223,6 +225,9 @@ def undistort_keypoints(self):
     return self.mvKeysUn
 
 
+_DOUBLE_OR_INT = (float, int, np.float64)
+
+
 def assign_features_to_grid(self) -> None:
     """Frame.assign_features_to_grid + pos_in_grid (Frame.py:143-159) with the per-keypoint Python loop
     replaced by array operations: the same positions (np.round of the same float64 expression), the same
@@ -241,9 +246,16 @@ def assign_features_to_grid(self) -> None:
         pts = kxy[1]  # extract_orb's copy of the same coordinates (mvKeys is the list it built)
     else:
         pts = np.fromiter((c for kp in kps for c in kp.pt), np.float64, count=2 * n).reshape(n, 2)
+    cols, rows = self.FRAME_GRID_COLS, self.FRAME_GRID_ROWS
+    f4 = (self.mnMinX, self.mnMinY, self.mfGridElementWidthInv, self.mfGridElementHeightInv)
+    if all(type(v) in _DOUBLE_OR_INT for v in f4) and type(cols) is int and type(rows) is int:
+        # doubles throughout: cells, CSR and the mGrid lists in one C pass (_pyhost.grid_assign)
+        self.mGrid, off, flat = pyhost().grid_assign(np.ascontiguousarray(pts, np.float64), *map(float, f4), cols, rows)
+        self._orbfe_grid = (id(self.mGrid), off, flat)
+        self._orbfe_pts = (kps, pts)
+        return
     px = np.round((pts[:, 0] - self.mnMinX) * self.mfGridElementWidthInv).astype(int)
     py = np.round((pts[:, 1] - self.mnMinY) * self.mfGridElementHeightInv).astype(int)
-    cols, rows = self.FRAME_GRID_COLS, self.FRAME_GRID_ROWS
     valid = (px >= 0) & (px < cols) & (py >= 0) & (py < rows)
     keep = np.flatnonzero(valid)
     cell = px[keep] * rows + py[keep]
@@ -251,9 +263,7 @@ def assign_features_to_grid(self) -> None:
     flat = keep[order].astype(np.int32)
     off = np.zeros(cols * rows + 1, np.int32)
     np.cumsum(np.bincount(cell, minlength=cols * rows), out=off[1:])
-    fl, o = flat.tolist(), off.tolist()
-    cells = [fl[a:b] for a, b in zip(o, o[1:])]  # one new list per cell, column-major
-    self.mGrid = [cells[i:i + rows] for i in range(0, cols * rows, rows)]
+    self.mGrid = pyhost().grid_lists(flat, off, cols, rows)  # a new list per cell, built in C
     self._orbfe_grid = (id(self.mGrid), off, flat)
     self._orbfe_pts = (kps, pts)  # the keypoint coordinates as doubles, for the matcher's grid queries
 

@@ -269,11 +269,10 @@ def _stride_ignoring_view(img: np.ndarray, nh: int, nw: int) -> np.ndarray:
     return flat[p - lo:p - lo + nh * nw].reshape(nh, nw)
 
 
-KP_FIELDS = ("x", "y", "size", "angle", "response", "octave")
-
-
 def keypoint_tuples(kps: np.ndarray) -> list:
     """cv::KeyPoint tuples (x, y, size, angle, response, octave) as the reference caster builds them
-    (opencv_type_casters.h:106-108): Python floats (exact f32 values) and an int.  Built from one list per
-    field (zip of contiguous columns: ~40 % faster than the structured array's tolist)."""
-    return list(zip(*[kps[f].tolist() for f in KP_FIELDS]))
+    (opencv_type_casters.h:106-108): Python floats (exact f32 values) and an int, built in C
+    (`_pyhost.keypoint_tuples`; the structured array's tolist is ~3x slower)."""
+    if kps.dtype != KP_DTYPE:
+        raise TypeError("keypoint records must have the orbfe_keypoint dtype")
+    return _lib.pyhost().keypoint_tuples(np.ascontiguousarray(kps))
