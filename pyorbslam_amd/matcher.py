@@ -32,6 +32,7 @@ import ctypes as C
 import operator
 import threading
 import weakref
+from collections import deque
 from itertools import compress, repeat
 
 import numpy as np
@@ -487,7 +488,9 @@ class ORBMatcher:
         # BLAS product as `Rcw @ x3Dw`, element-wise arithmetic in the reference's order and dtypes)
         lmps, lout, n_last = last_frame.mvpMapPoints, last_frame.mvbOutlier, last_frame.N
         if len(lmps) >= n_last and len(lout) >= n_last:
-            cand = [i for i, m, o in zip(range(n_last), lmps, lout) if m and not o]
+            # [i for i in range(n_last) if lmps[i] and not lout[i]] with C-level iteration (bool(m): the
+            # truth test `if m` makes; not o)
+            cand = list(compress(range(n_last), map(operator.and_, map(bool, lmps), map(operator.not_, lout))))
         else:  # the reference's indexing (and its IndexError)
             cand = [i for i in range(n_last) if lmps[i] and not lout[i]]
         pos = list(map(_WORLD_POS, map(lmps.__getitem__, cand)))
@@ -659,14 +662,14 @@ class ORBMatcher:
             lo, hi = octv - 1, octv + 1
         qx, iz = np.ascontiguousarray(u[sel]), np.ascontiguousarray(invzc[sel])
         off, idx = _grid_csr(cur, grid, qx, v[sel], radius, lo, hi)
-        pmps = [last.mvpMapPoints[i] for i in ci]
+        pmps = list(map(last.mvpMapPoints.__getitem__, ci))
         rows, off2, dist = self._nonempty(off, idx, pmps, cur.mDescriptors)
         n_matches = 0
         rot_hist = [[] for _ in range(HISTO_LENGTH)]
         factor = 1.0 / HISTO_LENGTH
         if len(rows):
             rl = rows.tolist()
-            q_obs = _obs_flags([pmps[r] for r in rl])
+            q_obs = _obs_flags(list(map(pmps.__getitem__, rl)))
             blocked = _blocked(cur)
             best = np.empty(len(rl), np.int32)
             qu, qz, qrad = (np.ascontiguousarray(a[rows], np.float64) for a in (qx, iz, radius))  # held across the call
@@ -674,8 +677,8 @@ class ORBMatcher:
                  ptr(u_right), ptr(blocked), n_frame, float(cur.mbf), TH_HIGH, ptr(best))
             hit = np.flatnonzero(best >= 0)
             bl = best[hit].tolist()
-            for j, b in zip(hit.tolist(), bl):
-                cur.mvpMapPoints[b] = pmps[rl[j]]
+            # cur.mvpMapPoints[b] = pmps[rl[j]] in query order, the list's own __setitem__ mapped in C
+            deque(map(cur.mvpMapPoints.__setitem__, bl, map(pmps.__getitem__, map(rl.__getitem__, hit.tolist()))), 0)
             n_matches += len(bl)
             if self.mbCheckOrientation and bl:  # ORBMatcher.py:374-382
                 la, ca = _angles(last), _angles(cur)
@@ -693,8 +696,8 @@ class ORBMatcher:
                             rot += 360.0
                         bin_idx = round(rot * factor)
                         bins.append(0 if bin_idx == HISTO_LENGTH else bin_idx)
+                assert not bins or 0 <= min(bins) <= max(bins) < HISTO_LENGTH  # ORBMatcher.py's per-bin assert
                 for b, k in zip(bl, bins):
-                    assert 0 <= k < HISTO_LENGTH
                     rot_hist[k].append(b)
         if self.mbCheckOrientation:
             ind1, ind2, ind3 = self.compute_three_maxima(rot_hist, HISTO_LENGTH)

@@ -1,5 +1,6 @@
 """Debug aid: cProfile of the C3 replay's timed calls alone (the Frame constructor, search_by_projection_f_f /
-_f_p) on the GPU box; prints their wall times and the profile of those calls only (argv[2]: sort key)."""
+_f_p) on the GPU box; prints their wall times and the profile of those calls only (argv[2]: sort key,
+argv[3]: profile only this section: frame, f_f or f_p)."""
 import cProfile
 import json
 import pstats
@@ -23,9 +24,12 @@ T = {"f_f": [], "f_p": [], "frame": []}
 on = [False]
 
 
+ONLY = sys.argv[3] if len(sys.argv) > 3 else None
+
+
 class PM(ORBMatcher):
     def search_by_projection_f_f(self, *a):
-        if on[0]:
+        if on[0] and ONLY in (None, "f_f"):
             prof.enable()
         t = time.perf_counter()
         try:
@@ -35,7 +39,7 @@ class PM(ORBMatcher):
             T["f_f"].append(time.perf_counter() - t)
 
     def search_by_projection_f_p(self, *a):
-        if on[0]:
+        if on[0] and ONLY in (None, "f_p"):
             prof.enable()
         t = time.perf_counter()
         try:
@@ -47,7 +51,7 @@ class PM(ORBMatcher):
 
 class DropInFrame(H.SeqFrame):
     def __init__(self, *a, **k):
-        if on[0]:
+        if on[0] and ONLY in (None, "frame"):
             prof.enable()
         t = time.perf_counter()
         try:
