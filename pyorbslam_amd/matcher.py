@@ -154,6 +154,9 @@ _IN_VIEW = operator.attrgetter("mbTrackInView")
 _IS_BAD = operator.methodcaller("is_bad")
 _VIEW_COS = operator.attrgetter("mTrackViewCos")
 _TRACK_LEVEL = operator.attrgetter("mnTrackScaleLevel")
+_PROJ_X = operator.attrgetter("mTrackProjX")
+_PROJ_Y = operator.attrgetter("mTrackProjY")
+_PROJ_XR = operator.attrgetter("mTrackProjXR")
 _WORLD_POS = operator.methodcaller("get_world_pos")
 _DESCRIPTOR = operator.methodcaller("get_descriptor")
 
@@ -601,13 +604,13 @@ class ORBMatcher:
         if lo_hi.min() < -len(sf) or lo_hi.max() >= len(sf):
             return None
         qr = np.array(rads, np.float64) * np.array(sf, np.float64)[lo_hi]  # r * mvScaleFactors[level], doubles
-        qx = _f64_array([p.mTrackProjX for p in pmps])
+        qx = _f64_array(list(map(_PROJ_X, pmps)))
         if qx is None:
             return None
-        qy = _f64_array([p.mTrackProjY for p in pmps])
+        qy = _f64_array(list(map(_PROJ_Y, pmps)))
         if qy is None:
             return None
-        xr_all = [p.mTrackProjXR for p in pmps]
+        xr_all = list(map(_PROJ_XR, pmps))
         xr_arr = _f64_array(xr_all)
         if xr_arr is None:
             return None
@@ -627,16 +630,15 @@ class ORBMatcher:
         rl = rows.tolist()
         xr = np.ascontiguousarray(xr_arr[rows])
         rs = np.ascontiguousarray(qr[rows])
-        q_obs = _obs_flags([pmps[r] for r in rl])
+        q_obs = _obs_flags(list(map(pmps.__getitem__, rl)))
         blocked = _blocked(frame)
         best = np.empty(len(rl), np.int32)
         call("orbfe_select_f_p", len(rl), ptr(off2), ptr(idx), ptr(dist), ptr(xr), ptr(rs), ptr(grid[4]), ptr(q_obs),
              ptr(u_right), ptr(blocked), n_frame, float(self.mfNNratio), TH_HIGH, ptr(best))
-        n_matches = 0
-        for j in np.flatnonzero(best >= 0).tolist():
-            frame.mvpMapPoints[int(best[j])] = pmps[rl[j]]
-            n_matches += 1
-        return n_matches
+        hit = np.flatnonzero(best >= 0).tolist()
+        # frame.mvpMapPoints[best[j]] = pmps[rl[j]] in query order, the list's own __setitem__ mapped in C
+        deque(map(frame.mvpMapPoints.__setitem__, best[hit].tolist(), map(pmps.__getitem__, map(rl.__getitem__, hit))), 0)
+        return len(hit)
 
     def _f_f_native(self, cur, last, th, b_forward, b_backward, cand, sel, u, v, invzc):
         grid = _frame_grid(cur)
