@@ -125,11 +125,14 @@ class ORBextractor:
     def _cap(self) -> int:
         return int(self._params.nfeatures) + 8 * self._nlevels + 64
 
-    def _set_result(self, kps: np.ndarray, desc: np.ndarray, n: int, extracted: bool) -> None:
+    def _set_result(self, kps: np.ndarray, desc: np.ndarray, n: int, extracted: bool, exact: bool = False) -> None:
+        """exact: kps / desc are already the n records (fresh arrays), kept without a copy."""
         self._extracted = extracted
         if n == 0:
             # _descriptors.release() / never created -> empty cv::Mat -> (0, 0) array
             self._kps, self._desc = kps[:0].copy(), np.zeros((0, 0), np.uint8)
+        elif exact:
+            self._kps, self._desc = kps, desc
         else:
             self._kps, self._desc = kps[:n].copy(), desc[:n].copy()
 
@@ -187,14 +190,14 @@ class ORBextractor:
             self._frame_hw, self._frame_shapes = (h, w), None
         call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
              int(bool(want_pyramid)))
-        cap = self._cap()
         out = []
         for side, ex in ((0, self), (1, right_extractor)):
-            kps = np.empty(cap, KP_DTYPE)
-            desc = np.empty((cap, 32), np.uint8)
-            n = C.c_int32()
-            call("orbfe_frame_fetch", self._h, side, ptr(kps), ptr(desc), cap, C.byref(n))
-            ex._set_result(kps, desc, n.value, w > 0 and h > 0)
+            n = C.c_int32()  # the count first (no copy), then the records straight into exact-size arrays
+            call("orbfe_frame_fetch", self._h, side, None, None, 2 ** 31 - 1, C.byref(n))
+            kps = np.empty(n.value, KP_DTYPE)
+            desc = np.empty((n.value, 32), np.uint8)
+            call("orbfe_frame_fetch", self._h, side, ptr(kps), ptr(desc), n.value, C.byref(n))
+            ex._set_result(kps, desc, n.value, w > 0 and h > 0, exact=True)
             ex._pyr_src = (self, side) if w > 0 and h > 0 else None
             ex._pyr_cache = None
             ex.stereo_result = None
