@@ -102,10 +102,11 @@ def extract_orb(self, flag, image) -> None:
             self.mvKeys_, self.mDescriptors = left.operator_kd(image)
         self.mvKeys = list(starmap(KeyPoint, self.mvKeys_))  # [KeyPoint(*kp) for kp in mvKeys_], Frame.py:117
         if isinstance(left, ORBextractor) and len(left.last_keypoints) == len(self.mvKeys):
-            # the keypoints' pt as doubles straight from the extractor's float32 fields (the values the
-            # KeyPoints were built from), for assign_features_to_grid while mvKeys is still this list
+            # the keypoints' pt, octave and angle straight from the extractor's fields (the values the
+            # KeyPoints were built from), for assign_features_to_grid and the matcher while mvKeys is this list
             kl = left.last_keypoints
-            self._orbfe_kxy = (self.mvKeys, np.stack((kl["x"], kl["y"]), axis=1).astype(np.float64))
+            self._orbfe_kxy = (self.mvKeys, np.stack((kl["x"], kl["y"]), axis=1).astype(np.float64),
+                               kl["octave"].astype(np.int32), kl["angle"].astype(np.float64))
     elif flag == 1:
         pend = right.take_pending(image) if isinstance(right, ORBextractor) else None
         if pend is not None:

@@ -211,7 +211,11 @@ def _octaves(frame) -> np.ndarray:
         ent = None
     if ent is not None and ent[0] == key:
         return ent[1]
-    arr = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
+    kxy = getattr(frame, "_orbfe_kxy", None)  # frame.extract_orb's copy of the fields mvKeys was built from
+    if kxy is not None and kxy[0] is kps and len(kxy[2]) == len(kps) and _kp_field_ok(kps, kxy[2], "octave", int):
+        arr = kxy[2]
+    else:
+        arr = np.fromiter((k.octave for k in kps), np.int32, count=len(kps))
     try:
         _octave_cache[frame] = (key, arr)
     except TypeError:
@@ -220,6 +224,15 @@ def _octaves(frame) -> np.ndarray:
 
 
 _angle_cache = weakref.WeakKeyDictionary()
+
+
+def _kp_field_ok(kps, arr, name, typ) -> bool:
+    """The KeyPoint class kept the extractor's values as given (spot check of the first and last keypoint:
+    the type and the value of field `name`), so the extractor's array stands for the KeyPoints' fields."""
+    if len(kps) == 0:
+        return True
+    a, b = getattr(kps[0], name), getattr(kps[-1], name)
+    return type(a) is typ and type(b) is typ and a == arr[0] and b == arr[-1]
 
 
 def _angles(frame):
@@ -234,9 +247,13 @@ def _angles(frame):
     if ent is not None and ent[0] == key:
         return ent[1]
     arr = None
-    angles = list(map(_ANGLE, kps))
-    if set(map(type, angles)) <= _F64_SET:
-        arr = np.array(angles, np.float64)
+    kxy = getattr(frame, "_orbfe_kxy", None)
+    if kxy is not None and kxy[0] is kps and len(kxy[3]) == len(kps) and _kp_field_ok(kps, kxy[3], "angle", float):
+        arr = kxy[3]  # the KeyPoints' angles are the Python floats of these float32 values
+    else:
+        angles = list(map(_ANGLE, kps))
+        if set(map(type, angles)) <= _F64_SET:
+            arr = np.array(angles, np.float64)
     try:
         _angle_cache[frame] = (key, arr)
     except TypeError:
