@@ -679,6 +679,21 @@ __device__ __forceinline__ uint32_t fast_m_pair(const uint32_t* R) {
 
 __device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
 
+// o +/- (this lane's bit of the lane mask m): one v_addc / v_subb with the mask as the carry (the compiler's
+// form of o + (int)inverse_ballot(m) is a v_cndmask and an add)
+__device__ __forceinline__ int fd_plus_bit(int o, uint64_t m) {
+    int r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(o), "s"(m));
+    return r;
+}
+__device__ __forceinline__ int fd_minus_bit(int o, uint64_t m) {
+    int r;
+    uint64_t co;
+    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(o), "s"(m));
+    return r;
+}
+
 // cells per k_detect wavefront: 4 (the next cell's ROI loads overlap this one), or 1 for batches too small to
 // give the chip >= 8 waves per CU that way (a frame pair: 610 waves of 4 cells, 2 440 of one)
 constexpr int kFdCells = 4;
@@ -844,18 +859,19 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 bound_at((const uint32_t*)(roi + (min(y, wh - 1) + 3) * RP + x4 + 4),
                          __builtin_amdgcn_sicmp(i, nquad, 40), __builtin_amdgcn_sicmp(x4, xl, 32), ca, cb, aa, ab);
             };
-            // a lane's second entry goes after its first: its offset counts the first-entry bits at or below
-            // the lane, mbcnt(b0 >> 1) + bit 0 of b0 (uniform), on top of the second-entry bits below it
+            // entries in lane order, a lane's first before its second: the lane's first goes after every entry
+            // of the lanes below it (one mbcnt chain over both masks, seeded with the queue length), its second
+            // one further when it has a first
+            auto below2 = [](uint64_t m0, uint64_t m1, int base) {
+                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1,
+                       __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, base))));
+            };
             auto emit = [&](int n, uint64_t b0, uint64_t b1, uint64_t a0, uint64_t a1) {
                 const bool ca = __builtin_amdgcn_inverse_ballot_w64(b0), cb = __builtin_amdgcn_inverse_ballot_w64(b1);
-                const int n1 = lanes_below(b1);
                 const uint16_t e = (uint16_t)n;
-                if (ca) pq[npq + lanes_below(b0) + n1] = e;
-                const uint64_t b0s = b0 >> 1;
-                if (cb)
-                    pq[npq + (int)(b0 & 1) +
-                       (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0s >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0s, n1))] =
-                        (uint16_t)(e + 2);
+                const int o = below2(b0, b1, npq);
+                if (ca) pq[o] = e;
+                if (cb) pq[fd_plus_bit(o, b0)] = (uint16_t)(e + 2);
                 npq += __popcll(b0) + __popcll(b1);
                 if (two) {
                     const bool aa = __builtin_amdgcn_inverse_ballot_w64(a0), ab = __builtin_amdgcn_inverse_ballot_w64(a1);
@@ -863,13 +879,9 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     // both counts only grow: once the queues would meet they stay met (collide below), and A
                     // stops writing so that B stays intact for the one-pass path
                     if (npq + npa + na <= cap) {
-                        const int m1 = lanes_below(a1);
-                        if (aa) pq[cap - 1 - npa - lanes_below(a0) - m1] = e;
-                        const uint64_t a0s = a0 >> 1;
-                        if (ab)
-                            pq[cap - 1 - npa - (int)(a0 & 1) -
-                               (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(a0s >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0s, m1))] =
-                                (uint16_t)(e + 2);
+                        const int oa = cap - 1 - below2(a0, a1, npa);
+                        if (aa) pq[oa] = e;
+                        if (ab) pq[fd_minus_bit(oa, a0)] = (uint16_t)(e + 2);
                     }
                     npa += na;
                 }
@@ -971,7 +983,10 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                     const int o = t + lanes_below(ba) + lanes_below(bb);
                     // slot_cap holds by the strict NMS (no two kept pixels are 8-neighbours); never write past it
                     if (ka && o < cg.slot_cap) dst[o] = reca;
-                    if (kb && o + (int)ka < cg.slot_cap) dst[o + (int)ka] = recb;
+                    if (kb) {
+                        const int ob = fd_plus_bit(o, ba);
+                        if (ob < cg.slot_cap) dst[ob] = recb;
+                    }
                     t += __popcll(ba) + __popcll(bb);
                 };
                 uint64_t ba, bb;
