@@ -2468,24 +2468,23 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                           __builtin_amdgcn_alignbyte(w[4 * k + 3], w[4 * k + 2], rsh), __builtin_amdgcn_alignbyte(w[4 * k + 4], w[4 * k + 3], rsh)};
         }
     };
-    auto stage_border = [&](int cx, int cy) {  // reflect-101 at the level border, byte by byte
-        uint8_t* sb = (uint8_t*)src;
-        constexpr int NB = (kSrcRows * 4 * kSrcDw + 63) / 64, NR = 8;  // 33 bytes per lane, 8 loads in flight
+    // reflect-101 at the level border: lane r stages window row r (its reflected level row, one offset per
+    // lane) from byte loads whose reflected column is wave-uniform (SGPR soffset), 16 bytes in flight at a time
+    auto stage_border = [&](int cx, int cy) {
+        const uint32_t ro = (uint32_t)(reflect101c(cy - 21 + it_r, Lh) * stride) + bias;
 #pragma unroll 1
-        for (int j0 = 0; j0 < NB; j0 += NR) {
-            uint32_t v[NR];
+        for (int q0 = 0; q0 < kSrcDw; q0 += 4) {
+            uint32_t v[16];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const int i = min(lane + 64 * (j0 + k), kSrcRows * 4 * kSrcDw - 1);
-                const int r = i / (4 * kSrcDw), c = i - r * (4 * kSrcDw);
-                const int y = reflect101c(cy - 21 + r, Lh), x = reflect101c(cx - 25 + c, Lw);
-                v[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(y * stride + x) + bias, 0, 0);
-            }
+            for (int t = 0; t < 16; ++t)
+                v[t] = __builtin_amdgcn_raw_buffer_load_b8(rs, ro, (uint32_t)reflect101c(cx - 25 + 4 * q0 + t, Lw), 0);
+            uint4 u;
+            uint32_t* uw = (uint32_t*)&u;
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const int i = lane + 64 * (j0 + k);
-                if (i < kSrcRows * 4 * kSrcDw) sb[i] = (uint8_t)v[k];
-            }
+            for (int q = 0; q < 4; ++q)
+                uw[q] = __builtin_amdgcn_perm(v[4 * q + 1], v[4 * q], 0x0c0c0400u) |
+                        __builtin_amdgcn_perm(v[4 * q + 3], v[4 * q + 2], 0x04000c0cu);
+            if (lane < kSrcRows) *(uint4*)(src + kSrcDw * lane + q0) = u;
         }
     };
     int cx = 0, cy = 0;
