@@ -1557,7 +1557,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
 // scratch.  Equal-size ties of the careful phase resolve by creation order, as in k_octree.
 constexpr int kObThreads = 256;
 #ifndef ORBFE_OB_BATCH
-#define ORBFE_OB_BATCH 8
+#define ORBFE_OB_BATCH 4
 #endif
 constexpr int kObBatch = ORBFE_OB_BATCH;    // slot loads in flight per thread in the first sweep
 constexpr uint32_t kObDeep = 0x80000000u;   // bin flag: holds nodes deeper than D0 (deep sweep / final map)
