@@ -852,6 +852,13 @@ def main():
                                       pairs_per_s / world if pairs_per_s else None, args.roofline_steps))
         if gather is not None:
             out["with_gather"] = gather
+        if c4 is None and strong and args.total_pairs == C4_TOTAL_PAIRS and pairs_per_s is not None:
+            # --total-pairs 64 IS C4: its line under the same key as the weak-scaling run's C4 block
+            c4 = {"total_pairs": C4_TOTAL_PAIRS, "pairs_per_gpu": P, "handles_per_gpu": n_handles,
+                  "value": out["value"], "unit": "pairs/s", "ms_per_step": out["ms_per_step"], "scaling": "strong",
+                  "what": "BASELINE configs[3]: this run's own step (--total-pairs 64, sharded over the ranks)"}
+            if gather is not None:
+                c4["with_gather"] = gather
         if c4 is not None:
             out["c4_strong"] = c4
         if share is not None:

@@ -16,6 +16,7 @@ constexpr int kBorder = kEdge - 3; // minBorderX/Y (ORBextractor.cpp:772-773)
 constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
 constexpr int kPatchR = 21;        // descriptor patch radius: 18 (max rotated pattern offset) + 3 (blur)
 constexpr int kPatchD = 2 * kPatchR + 1;  // 43
+constexpr int kMaxLevelSide = 4095;  // level coordinates are 12-bit fields (FAST slots, level keypoints, compact records)
 constexpr int kMaxCellRoi = 64;    // max cell ROI side (wCell+6, hCell+6); checked on the host
 
 // One pyramid level of one image geometry.

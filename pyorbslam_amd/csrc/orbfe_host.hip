@@ -113,6 +113,7 @@ struct orbfe_ctx {
     struct GraphEntry {
         std::vector<uint64_t> key;
         hipGraphExec_t exec;
+        hipEvent_t done;  // recorded after every launch of exec: retire() waits for it before destroying
     };
     std::vector<GraphEntry> graphs;
     int64_t graph_launches = 0, graph_captures = 0;
@@ -141,13 +142,23 @@ struct orbfe_ctx {
     size_t fo_count = 0, fo_kps = 0, fo_desc = 0, fo_uR = 0, fo_depth = 0, fo_status = 0, fo_match = 0, fo_ovf = 0,
            fo_shear = 0;
 
+    // An executable graph may still be queued or running on the caller's stream when it is evicted or
+    // dropped (nothing synchronises between batch enqueues): wait for its last launch before destroying it
+    // (destroying a running executable is not specified to be safe).
+    static void retire(GraphEntry& e) {
+        if (e.done) {
+            (void)hipEventSynchronize(e.done);
+            (void)hipEventDestroy(e.done);
+        }
+        (void)hipGraphExecDestroy(e.exec);
+    }
     void drop_graphs() {
-        for (GraphEntry& e : graphs) (void)hipGraphExecDestroy(e.exec);
+        for (GraphEntry& e : graphs) retire(e);
         graphs.clear();
         ++gen;
     }
     ~orbfe_ctx() {
-        for (GraphEntry& e : graphs) (void)hipGraphExecDestroy(e.exec);
+        for (GraphEntry& e : graphs) retire(e);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -376,7 +387,9 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         Lg.inv_scale = c.isf[l];
         Lg.w = round_even_f((float)W * c.isf[l]);
         Lg.h = round_even_f((float)H * c.isf[l]);
-        if (Lg.w < 1 || Lg.h < 1 || Lg.w > 4095 || Lg.h > 4095)
+        // kMaxLevelSide: the 12-bit level coordinates of the FAST slots, the level keypoints and the compact
+        // gather records (k_detect, k_octree_bins, k_pack_compact)
+        if (Lg.w < 1 || Lg.h < 1 || Lg.w > kMaxLevelSide || Lg.h > kMaxLevelSide)
             throw Error(ORBFE_EINVAL, "level size out of range (1..4095 px per side)");
         if (Lg.w <= kEdge || Lg.h <= kEdge)
             throw Error(ORBFE_EINVAL, "image too small: a pyramid level is not wider than the 19 px reflect border");
@@ -857,6 +870,7 @@ void run_enqueue(orbfe_ctx& c, int kind, std::vector<uint64_t> key, hipStream_t 
     for (orbfe_ctx::GraphEntry& e : c.graphs)
         if (e.key == key) {
             HIPCK(hipGraphLaunch(e.exec, s));
+            HIPCK(hipEventRecord(e.done, s));
             ++c.graph_launches;
             return;
         }
@@ -874,13 +888,19 @@ void run_enqueue(orbfe_ctx& c, int kind, std::vector<uint64_t> key, hipStream_t 
     const hipError_t e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
     (void)hipGraphDestroy(gr);
     HIPCK(e);
+    hipEvent_t done = nullptr;
+    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGraphExecDestroy(ex);
+        throw Error(ORBFE_EHIP, "hipEventCreateWithFlags failed");
+    }
     if (c.graphs.size() >= kMaxGraphs) {
-        (void)hipGraphExecDestroy(c.graphs.front().exec);
+        orbfe_ctx::retire(c.graphs.front());
         c.graphs.erase(c.graphs.begin());
     }
-    c.graphs.push_back({std::move(key), ex});
+    c.graphs.push_back({std::move(key), ex, done});
     ++c.graph_captures;
     HIPCK(hipGraphLaunch(ex, s));
+    HIPCK(hipEventRecord(done, s));
     ++c.graph_launches;
 }
 
@@ -1392,6 +1412,9 @@ int orbfe_batch_pack_compact_device(orbfe_handle h, uint8_t* d_records, int64_t 
         if (rec_bytes != compact_record_bytes(h->geo.kp_cap))
             throw Error(ORBFE_EINVAL, "record size does not match kp_cap");
         if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
+        for (int l = 0; l < h->geo.nlevels; ++l)  // the compact format's 12-bit level coordinates (k_pack_compact)
+            if (h->geo.lv[l].w > kMaxLevelSide || h->geo.lv[l].h > kMaxLevelSide)
+                throw Error(ORBFE_EINVAL, "compact records hold level coordinates below 4096 px only");
         hipPointerAttribute_t pa{};
         if (hipPointerGetAttributes(&pa, d_records) != hipSuccess || pa.type != hipMemoryTypeDevice) {
             (void)hipGetLastError();

@@ -3238,17 +3238,31 @@ size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
 // gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB on request.  Raised (never lowered) once per
 // process and kernel, when a geometry is built (orbfe_host.hip prepare_kernels): launches, which may be
 // inside a graph capture, only check.
-static int g_lds_attr[3] = {64 * 1024, 64 * 1024, 64 * 1024};  // k_octree_bins<256>, k_octree, k_octree_bins<1024>
-static int g_lds_cascade = 64 * 1024;                // k_resize_cascade
+// hipFuncSetAttribute acts on the current device, so the raised limits are remembered per device
+// (a process with handles on two GPUs must raise them on each).
+constexpr int kMaxDevices = 64;
+struct LdsAttr {
+    int octree[3] = {64 * 1024, 64 * 1024, 64 * 1024};  // k_octree_bins<256>, k_octree, k_octree_bins<1024>
+    int cascade = 64 * 1024;                            // k_resize_cascade
+};
+static LdsAttr g_lds[kMaxDevices];
 static std::mutex g_lds_mu;
+
+static LdsAttr* lds_attr() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    return &g_lds[dev];
+}
 
 hipError_t prepare_resize_cascade(int lds_bytes) {
     std::lock_guard<std::mutex> lk(g_lds_mu);
-    if (lds_bytes <= g_lds_cascade) return hipSuccess;
+    LdsAttr* a = lds_attr();
+    if (!a) return hipErrorInvalidDevice;
+    if (lds_bytes <= a->cascade) return hipSuccess;
     if (lds_bytes > 160 * 1024) return hipErrorInvalidValue;
     const hipError_t e =
         hipFuncSetAttribute((const void*)k_resize_cascade, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    if (e == hipSuccess) g_lds_cascade = lds_bytes;
+    if (e == hipSuccess) a->cascade = lds_bytes;
     return e;
 }
 
@@ -3256,20 +3270,29 @@ hipError_t prepare_octree(const Geo& g, int maxcell) {
     const size_t need[3] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell), octree_bins_lds_bytes(g, maxcell)};
     const void* fn[3] = {(const void*)k_octree_bins<kObThreads>, (const void*)k_octree, (const void*)k_octree_bins<1024>};
     std::lock_guard<std::mutex> lk(g_lds_mu);
+    LdsAttr* a = lds_attr();
+    if (!a) return hipErrorInvalidDevice;
     for (int k = 0; k < 3; ++k) {
-        if ((int)need[k] <= g_lds_attr[k] || need[k] > 160 * 1024) continue;
+        if ((int)need[k] <= a->octree[k] || need[k] > 160 * 1024) continue;
         const hipError_t e = hipFuncSetAttribute(fn[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[k]);
         if (e != hipSuccess) return e;
-        g_lds_attr[k] = (int)need[k];
+        a->octree[k] = (int)need[k];
     }
     return hipSuccess;
+}
+
+// the limit raised on the current device for kernel k (0..2 octree, 3 cascade)
+static int lds_limit(int k) {
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    const LdsAttr* a = lds_attr();
+    return !a ? 0 : k < 3 ? a->octree[k] : a->cascade;
 }
 
 hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                                  const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
                                  int lds_bytes, int n_images, hipStream_t s, int* zero_word) {
     if (g.nlevels < 2 || n_images <= 0) return hipSuccess;
-    if (lds_bytes > g_lds_cascade) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
+    if (lds_bytes > lds_limit(3)) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
     hipLaunchKernelGGL(k_resize_cascade, dim3(n_strips, n_images), dim3(512), (size_t)lds_bytes, s, g, in, in_pitch, ws,
                        xt, yt, strips, off_b, off_x, zero_word);
     return hipGetLastError();
@@ -3280,7 +3303,7 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
     if (g.oct_v == 0) {
         const size_t lds = octree_bins_lds_bytes(g, maxcell);
-        if ((int)lds > g_lds_attr[0] || (int)lds > g_lds_attr[2]) return hipErrorInvalidConfiguration;  // prepare_octree
+        if ((int)lds > lds_limit(0) || (int)lds > lds_limit(2)) return hipErrorInvalidConfiguration;  // prepare_octree
         // 1 024 threads for small batches (variant 1 / 2 force 256 / 1 024, tools/microbench.py)
         const bool wide = variant == 2 || (variant != 1 && n_images < kSmallBatchImages);
         if (wide)
@@ -3292,7 +3315,7 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
-    if ((int)lds > g_lds_attr[1]) return hipErrorInvalidConfiguration;
+    if ((int)lds > lds_limit(1)) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL(k_octree, dim3(n_images, g.nlevels), dim3(kOctThreads), lds, s, g, cells, cell_count, slots, kd, kn,
                        lvl_kp, lvl_count, overflow, maxcell, variant, prof);
     return hipGetLastError();
@@ -3397,7 +3420,9 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a, uint8_t* __restrict__ 
 // (cap x 32 B) | u_right, depth (cap x f32) | scores L, R (cap x u8) | status (cap x i8): 8 + 91 cap bytes
 // against 8 + 121 cap.  A keypoint's x, y, size and response follow from (x, y, octave, score) on the host
 // exactly as k_orb computed them (x = f32(level x) * scale[octave]; the level coordinate is recovered here
-// as rint(x * inv_scale), exact for coordinates < 2^22).
+// as rint(x * inv_scale), exact for coordinates < 2^22).  The record keeps 12 bits per level coordinate and 8
+// bits of response: exact only while every level is at most 4 095 px per side (build_geometry's limit,
+// kMaxLevelSide; orbfe_batch_pack_compact_device re-checks it) and the FAST score M - 1 <= 254 (u8 pixels).
 __global__ __launch_bounds__(256) void k_pack_compact(PackArgs a, CompactScales sc, uint8_t* __restrict__ out, int pair0) {
     const int p = blockIdx.y, gp = pair0 + p, t = blockIdx.x * 256 + threadIdx.x, nt = gridDim.x * 256;
     uint8_t* rec = out + (int64_t)p * a.rec_bytes;

@@ -112,8 +112,9 @@ def unpack_compact(kp_cap: int, rec: np.ndarray, scales) -> dict:
 
 
 def gather_buffer(world: int, records):
-    """dst's receive buffer for gather_records: one (world * local_pairs, record_bytes) tensor per (shape,
-    dtype, device), allocated on first use and reused by every later gather of that shape."""
+    """A reusable receive buffer for gather_records(out=...): one (world * local_pairs, record_bytes) tensor per
+    (shape, dtype, device), allocated on first use and returned again for every later request of that shape —
+    whoever passes it as `out` gets it overwritten by the next such gather (clear_gather_buffers frees them)."""
     import torch
     key = (world, tuple(records.shape), records.dtype, str(records.device))
     buf = _GATHER_BUF.get(key)
@@ -124,19 +125,27 @@ def gather_buffer(world: int, records):
     return buf
 
 
+def clear_gather_buffers() -> None:
+    """Drop the buffers gather_buffer keeps for reuse."""
+    _GATHER_BUF.clear()
+
+
 def gather_records(records, dst: int = 0, out=None):
     """records: (local_pairs, record_bytes) uint8 torch tensor of this rank — on the GPU with backend "nccl"
     (RCCL over xGMI), on the CPU with gloo.  Every rank must pass the same shape (the batched-frames mode
     gives every rank the same pair count; pad otherwise).  One collective, a gather to `dst` straight into
-    rank-major slices of one preallocated buffer (`out`, or gather_buffer's; no per-rank tensors, no
-    concatenation): returns that (world * local_pairs, record_bytes) tensor on dst — global pair order —,
-    None elsewhere.  The returned buffer is reused by the next gather of the same shape."""
+    rank-major slices of one receive buffer (no per-rank tensors, no concatenation): returns that
+    (world * local_pairs, record_bytes) tensor on dst — global pair order —, None elsewhere.  The buffer is
+    `out` when given (e.g. gather_buffer's reusable one, which the next gather into it overwrites), else a new
+    tensor that belongs to the caller (no silent aliasing across gathers)."""
+    import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
     if world == 1:
         return records
     if rank == dst:
-        full = gather_buffer(world, records) if out is None else out
+        full = (torch.empty((world * records.shape[0],) + tuple(records.shape[1:]), dtype=records.dtype,
+                            device=records.device) if out is None else out)
         if tuple(full.shape) != (world * records.shape[0],) + tuple(records.shape[1:]):
             raise ValueError("gather output buffer has the wrong shape")
         parts = list(full.view((world,) + tuple(records.shape)).unbind(0))  # contiguous rank slices
@@ -205,7 +214,10 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
         t0 = time.perf_counter()
         pack_device(frontends, counts, buf, compact)
         # RCCL gathers the device buffer in place; a gloo rehearsal (several ranks on one GPU) stages it
-        full = gather_records(buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu(), 0)
+        src = buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu()
+        # the one receive buffer of this shape, reused across the repetitions (allocated outside the timing
+        # by the warm-up repetition)
+        full = gather_records(src, 0, out=gather_buffer(world, src) if rank == 0 and world > 1 else None)
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()

@@ -415,18 +415,28 @@ class ORBMatcher:
         """The searched map points of search_by_projection_f_p (tracked in view, then not bad: the reference's
         two `continue`s in its order), their predicted levels and radii, with the per-point attribute reads
         and calls as map() over C-level getters.  The radius is ORBMatcher's own radius_by_viewing_cos
-        evaluated over an array of doubles (`vc > 0.998` in double, then `r *= th`); None (run the reference
-        loop) when the method is overridden, a view cosine is not a double (a float32 one compares in float32)
-        or th is not a Python number."""
+        evaluated over an array of doubles (`vc > 0.998` in double, then `r *= th`), or point by point when a
+        view cosine is not a double (a float32 one compares in float32); None (run the reference loop) when
+        the method is overridden or th is not a Python number."""
         if type(self).radius_by_viewing_cos is not ORBMatcher.radius_by_viewing_cos:
             return None
         if b_factor and type(th) not in (int, float):
             return None
         cand = list(compress(vp_map_points, map(_IN_VIEW, vp_map_points)))
         pmps = list(compress(cand, map(operator.not_, map(_IS_BAD, cand))))
-        vc = _f64_array(list(map(_VIEW_COS, pmps)))
+        cos = list(map(_VIEW_COS, pmps))
+        vc = _f64_array(cos)
         if vc is None:
-            return None
+            # not all doubles: the reference's per-point radius on the points already selected (ADVICE r4: no
+            # second mbTrackInView / is_bad() pass through the reference loop)
+            radius = self.radius_by_viewing_cos
+            rads = []
+            for c in cos:
+                r = radius(c)
+                if b_factor:
+                    r *= th
+                rads.append(r)
+            return pmps, list(map(_TRACK_LEVEL, pmps)), rads
         r = np.where(vc > 0.998, 2.5, 4.0)
         if b_factor:
             r = r * th
@@ -509,8 +519,9 @@ class ORBMatcher:
         lmps, lout, n_last = last_frame.mvpMapPoints, last_frame.mvbOutlier, last_frame.N
         if len(lmps) >= n_last and len(lout) >= n_last:
             # [i for i in range(n_last) if lmps[i] and not lout[i]] with C-level iteration (bool(m): the
-            # truth test `if m` makes; not o)
-            cand = list(compress(range(n_last), map(operator.and_, map(bool, lmps), map(operator.not_, lout))))
+            # truth test `if m` makes; `not lout[i]` only where lmps[i] is true, as the reference's `and`)
+            live = list(compress(range(n_last), map(bool, lmps)))
+            cand = list(compress(live, map(operator.not_, map(lout.__getitem__, live))))
         else:  # the reference's indexing (and its IndexError)
             cand = [i for i in range(n_last) if lmps[i] and not lout[i]]
         pos = list(map(_WORLD_POS, map(lmps.__getitem__, cand)))

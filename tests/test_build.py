@@ -65,3 +65,18 @@ def test_product_library_reads_no_environment():
     strs = subprocess.run(["strings", str(LIB)], check=True, capture_output=True, text=True).stdout
     names = set(re.findall(r"\bORBFE_[A-Z0-9_]+\b", strs)) - {"ORBFE_NSTAGES"}
     assert not names, f"liborbfe.so names environment-style knobs: {sorted(names)}"
+
+
+def test_gpu_push_carries_no_dev_variant_libraries():
+    """the tree gpurun pushes (tar with .gpurunignore's patterns) holds no development
+    variant library (pyorbslam_amd/_lib/variants/, tools/dbg/build_variant.sh builds) and still holds the
+    product library and the oracle checker the GPU runs load."""
+    if not shutil.which("tar"):
+        pytest.skip("tar missing")
+    r = subprocess.run(["tar", "-cvf", "/dev/null", "--exclude=./.git", "--exclude-from=.gpurunignore", "."],
+                       cwd=ROOT, check=True, capture_output=True, text=True)
+    names = [n.strip() for n in r.stdout.splitlines()]
+    assert not [n for n in names if "/_lib/variants" in n], "dev variant libraries travel to the GPU box"
+    if LIB.exists():
+        assert "./pyorbslam_amd/_lib/liborbfe.so" in names
+    assert "./bench.py" in names and "./tests/golden/" in names

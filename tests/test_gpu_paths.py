@@ -56,6 +56,39 @@ def test_graph_replay_equals_stream_path(n_pairs):
     assert kl.tobytes() == okl.tobytes() and np.array_equal(dl, odl)
 
 
+def test_graph_cache_eviction_with_new_inputs_every_step():
+    """with graphs on and a new input buffer every step, every enqueue captures a graph
+    and, past the 8-entry cache, evicts the oldest one while earlier steps are still queued on the caller's
+    stream (no synchronisation between enqueues).  Eviction must wait for the evicted executable's last
+    launch; the results of every step stay bit-exact to the stream path."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd.batch import StereoFrontEnd
+    n_pairs, steps = 2, 12
+    hosts = [synth.make_batch(n_pairs, seed0=700 + 10 * k) for k in range(steps)]
+    ref = StereoFrontEnd(max_pairs=n_pairs, lanes=1, graphs=False)
+    fe = StereoFrontEnd(max_pairs=n_pairs, lanes=1, graphs=True)
+    st = torch.cuda.Stream()
+    bufs = [torch.from_numpy(h).cuda() for h in hosts]  # 12 distinct pointers: 12 keys
+    torch.cuda.synchronize()
+    for d in bufs:  # back to back, no synchronisation: evictions overlap queued replays
+        fe.enqueue(d, n_pairs, stream_ptr=st.cuda_stream)
+    st.synchronize()
+    ref.enqueue(bufs[-1], n_pairs)
+    torch.cuda.synchronize()
+    _same_batches(ref, fe, n_pairs)
+    gs = fe.graph_stats()
+    assert gs["captures"] == steps and gs["launches"] == steps and gs["cached"] == 8, gs
+    assert fe.overflow() == 0
+    # a second round over the same pointers: all evicted keys are captured again, results still exact
+    for d in bufs:
+        fe.enqueue(d, n_pairs, stream_ptr=st.cuda_stream)
+    st.synchronize()
+    _same_batches(ref, fe, n_pairs)
+    kl, dl = fe.fetch_image(1)
+    okl, odl = O.OracleExtractor(**KITTI).extract(hosts[-1][1])
+    assert kl.tobytes() == okl.tobytes() and np.array_equal(dl, odl)
+
+
 def test_graph_frame_path_equals_stream_path():
     """orbfe_frame_extract (Frame(L, R) drop-in) replayed from its graph vs the stream path, over frames of a
     moving sequence (new image contents every call, the same staging buffers), with and without pyramids."""

@@ -331,9 +331,9 @@ def test_fp_python_float_xr_takes_the_float32_path(case, monkeypatch):
 
 def test_fp_inputs_equal_the_reference_loop():
     """search_by_projection_f_p's vectorised prologue (_f_p_inputs) keeps the reference loop's map points
-    (tracked in view, then not bad), levels and radii (ORBMatcher.py:224-232, `r *= th` when th != 1), and
-    declines (None) where the loop must run: a float32 view cosine (compares in float32), an overridden
-    radius_by_viewing_cos, a numpy th."""
+    (tracked in view, then not bad), levels and radii (ORBMatcher.py:224-232, `r *= th` when th != 1), takes
+    the radii point by point for a float32 view cosine (compares in float32), and declines (None) where the
+    loop must run: an overridden radius_by_viewing_cos, a numpy th."""
     from pyorbslam_amd.matcher import ORBMatcher
 
     class MP:
@@ -367,8 +367,20 @@ def test_fp_inputs_equal_the_reference_loop():
         assert got[0] == ref[0] and got[1] == ref[1]
         assert got[2] == ref[2] and all(type(v) is float for v in got[2])
     assert m._f_p_inputs(mps, np.float32(2.0), True) is None
+    # a float32 view cosine: the radii go point by point (the float32 comparison), over the points already
+    # selected — each point's mbTrackInView / is_bad() read once, as in the reference loop
     mps[0].mbTrackInView, mps[0]._bad, mps[0].mTrackViewCos = True, False, np.float32(0.998)
-    assert m._f_p_inputs(mps, 1, False) is None
+    calls = []
+    for p in mps:
+        p.is_bad = (lambda q=p: calls.append(q) or q._bad)
+    for th in (1, 2.5):
+        calls.clear()
+        got = m._f_p_inputs(mps, th, th != 1.0)
+        n_calls = len(calls)
+        ref = loop(m, th)
+        assert n_calls == sum(p.mbTrackInView for p in mps)
+        assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2]
+        assert [type(v) for v in got[2]] == [type(v) for v in ref[2]]
 
     class M2(ORBMatcher):
         def radius_by_viewing_cos(self, view_cos):

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--seq", action="store_true")
     ap.add_argument("--first", type=int, default=0, help="--seq: first frame")
+    ap.add_argument("--lanes", type=int, default=1, help="orbfe_set_lanes chunks (1: one launch of all images)")
     a = ap.parse_args()
     import torch
     from pyorbslam_amd import synth
@@ -26,7 +27,7 @@ def main():
         imgs = torch.from_numpy(np.stack([im for k in range(a.first, a.first + a.pairs) for im in sq.frame(k)])).cuda()
     else:
         imgs = torch.from_numpy(synth.make_batch(a.pairs)).cuda()
-    fe = StereoFrontEnd(max_pairs=a.pairs)
+    fe = StereoFrontEnd(max_pairs=a.pairs, lanes=a.lanes)
     fe.enqueue(imgs)
     torch.cuda.synchronize()
     n = 2 * a.pairs * 8 * 64
