@@ -48,6 +48,7 @@ def lib() -> C.CDLL:
         L.oracle_level_candidates.argtypes = [P, vp, C.c_int32, C.c_int32, vp, C.c_int32]
         L.oracle_octree.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp,
                                     C.c_int32]
+        L.oracle_octree_ties.argtypes = [P, vp, C.c_int32, C.c_int32, C.c_int32, vp]
         L.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
         L.oracle_fast_atan2.restype = C.c_float
         L.oracle_cosf.argtypes = [C.c_float]
@@ -105,6 +106,17 @@ class OracleExtractor:
             self._pyr.append(pyr[o:o + lw * lh].reshape(lh, lw).copy())
             o += lw * lh
         return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def octree_ties(self, image: np.ndarray) -> np.ndarray:
+        """SURVEY H1 per level: (straddle, tie_runs, careful_iters, run_len, run_divided) — see
+        oracle_octree_ties (orb_oracle.h)."""
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = image.shape
+        out = np.zeros((self.nlevels, 5), np.int32)
+        rc = lib().oracle_octree_ties(C.byref(self.p), _ptr(image), w, h, w, _ptr(out))
+        if rc != 0:
+            raise RuntimeError(f"oracle_octree_ties failed: {rc}")
+        return out
 
     def pyramid(self) -> list[np.ndarray]:
         return [p.copy() for p in self._pyr]

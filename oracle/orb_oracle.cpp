@@ -396,7 +396,20 @@ void divide(const std::vector<Cand>& K, const Node& nd, Node c[4]) {
         if (c[q].keys.size() == 1) c[q].noMore = true;
 }
 
-std::vector<int> distribute(const std::vector<Cand>& K, int minX, int maxX, int minY, int maxY, int N) {
+// how often the reference's own output depends on heap addresses.  The careful phase sorts
+// (size, ExtractorNode*) pairs (ORBextractor.cpp:683), so equal-size nodes are processed in address order:
+// *  tie_runs — runs of >= 2 equal-size nodes that the careful phase divided: their processing order, and
+//    so the order of their children in the list (push_front, :692-724) and of the level's keypoints, is
+//    address order (here: creation order);
+// *  straddle — the `>= N` break (:729-730) fell inside such a run: some of its nodes were divided and
+//    others not, so WHICH keypoints the level keeps depends on the addresses.
+struct TieStats {
+    int straddle = 0, tie_runs = 0, careful_iters = 0;
+    int run_len = 0, run_divided = 0;  // the straddled run: its equal-size nodes, how many of them were divided
+};
+
+std::vector<int> distribute(const std::vector<Cand>& K, int minX, int maxX, int minY, int maxY, int N,
+                            TieStats* ts = nullptr) {
     std::vector<int> result;
     if (K.empty() || maxY - minY <= 0 || maxX - minX <= 0) return result;
     const int nIni = (int)std::round((float)(maxX - minX) / (maxY - minY));
@@ -463,12 +476,32 @@ std::vector<int> distribute(const std::vector<Cand>& K, int minX, int maxX, int 
                 std::sort(todo.begin(), todo.end(), [](const std::pair<int, Node*>& a, const std::pair<int, Node*>& b) {
                     return a.first != b.first ? a.first < b.first : a.second->id < b.second->id;
                 });
+                int jb = 0;  // the last entry divided (entries jb .. end were divided, back to front)
+                bool broke = false;
                 for (int j = (int)todo.size() - 1; j >= 0; --j) {
                     Node c[4];
                     divide(K, *todo[j].second, c);
                     push_children(c, expand);
                     nodes.erase(todo[j].second->self);
-                    if ((int)nodes.size() >= N) break;
+                    jb = j;
+                    if ((int)nodes.size() >= N) { broke = true; break; }
+                }
+                if (ts && !todo.empty()) {
+                    ++ts->careful_iters;
+                    for (int j = jb; j < (int)todo.size();) {  // runs of equal size among the divided entries
+                        int e = j + 1;
+                        while (e < (int)todo.size() && todo[e].first == todo[j].first) ++e;
+                        ts->tie_runs += e - j >= 2;
+                        j = e;
+                    }
+                    if (broke && jb > 0 && todo[jb - 1].first == todo[jb].first) {
+                        ts->straddle = 1;
+                        int b = jb, e = jb;
+                        while (b > 0 && todo[b - 1].first == todo[jb].first) --b;
+                        while (e + 1 < (int)todo.size() && todo[e + 1].first == todo[jb].first) ++e;
+                        ts->run_len = e - b + 1;
+                        ts->run_divided = e - jb + 1;
+                    }
                 }
                 if ((int)nodes.size() >= N || (int)nodes.size() == prevSize) finish = true;
             }
@@ -639,6 +672,28 @@ int oracle_octree(const int32_t* xyr, int32_t n, int32_t minX, int32_t maxX, int
         out[3 * i + 2] = xyr[3 * sel[i] + 2];
     }
     return (int)sel.size();
+}
+
+int oracle_octree_ties(const orbfe_params* p, const uint8_t* img, int32_t w, int32_t h, int32_t stride, int32_t* ties) {
+    Config C;
+    if (!make_config(p, C) || !ties) return ORBFE_EINVAL;
+    for (int l = 0; l < 5 * C.nlevels; ++l) ties[l] = 0;
+    if (w <= 0 || h <= 0) return ORBFE_OK;
+    std::vector<Image> pyr;
+    build_pyramid(C, img, w, h, stride, pyr);
+    for (int l = 0; l < C.nlevels; ++l) {
+        std::vector<Cand> keys;
+        int minX, maxX, minY, maxY;
+        level_candidates(C, pyr[l], keys, minX, maxX, minY, maxY);
+        TieStats ts;
+        distribute(keys, minX, maxX, minY, maxY, C.nPerLevel[l], &ts);
+        ties[5 * l] = ts.straddle;
+        ties[5 * l + 1] = ts.tie_runs;
+        ties[5 * l + 2] = ts.careful_iters;
+        ties[5 * l + 3] = ts.run_len;
+        ties[5 * l + 4] = ts.run_divided;
+    }
+    return ORBFE_OK;
 }
 
 int oracle_extract(const orbfe_params* p, const uint8_t* img, int32_t w, int32_t h, int32_t stride,

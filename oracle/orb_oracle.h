@@ -53,6 +53,13 @@ int oracle_level_candidates(const orbfe_params* p, const uint8_t* lvl, int32_t w
 int oracle_octree(const int32_t* xyr, int32_t n, int32_t minX, int32_t maxX, int32_t minY, int32_t maxY,
                   int32_t N, int32_t* out, int32_t cap);
 
+/* SURVEY H1 tie report: per level l, ties[5l] = 1 if the careful phase's `>= N` break
+ * (ORBextractor.cpp:729-730) fell inside a run of equal-size nodes (which keypoints the reference keeps
+ * depends on heap addresses), ties[5l+1] = runs of >= 2 equal-size nodes the careful phase divided (their
+ * keypoints' ORDER depends on addresses), ties[5l+2] = careful-phase iterations, ties[5l+3] / [5l+4] = the
+ * straddled run's node count / how many of them were divided. */
+int oracle_octree_ties(const orbfe_params* p, const uint8_t* img, int32_t w, int32_t h, int32_t stride, int32_t* ties);
+
 /* cv::fastAtan2. */
 float oracle_fast_atan2(float y, float x);
 

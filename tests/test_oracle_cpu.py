@@ -11,6 +11,7 @@ import pytest
 from conftest import GOLDEN, KITTI, EUROC, BF, FX, STEREO_CASES, golden_case_images
 from oracle import oracle as O
 from oracle import stereo_oracle
+from pyorbslam_amd import synth
 
 
 # ----------------------------------------------------------------------------------- known answers
@@ -194,8 +195,10 @@ class _Node:
     __slots__ = ("keys", "x0", "y0", "x1", "y1", "nomore", "cid")
 
 
-def _octree_py(K, minX, maxX, minY, maxY, N):
-    """DistributeOctTree (ORBextractor.cpp:539-762) on a Python list; ties by creation id."""
+def _octree_py(K, minX, maxX, minY, maxY, N, reverse_ties=False):
+    """DistributeOctTree (ORBextractor.cpp:539-762) on a Python list; ties by creation id (the careful phase
+    divides the most recently created of equal-size nodes first), or with reverse_ties the oldest first — a
+    second admissible heap-address order."""
     if not K:
         return []
     nIni = int(math.floor(np.float32(maxX - minX) / np.float32(maxY - minY) + np.float32(0.5)))
@@ -247,7 +250,7 @@ def _octree_py(K, minX, maxX, minY, maxY, N):
         if len(nodes) + 3 * len(expand) > N:
             while True:
                 prev = len(nodes)
-                todo = sorted(expand, key=lambda n: (len(n.keys), n.cid))
+                todo = sorted(expand, key=lambda n: (len(n.keys), -n.cid if reverse_ties else n.cid))
                 expand = []
                 done = False
                 for n in reversed(todo):
@@ -340,3 +343,39 @@ def test_stereo_loop_restatement_matches_reference_golden(name, kitti_png):
     sd, vd = stereo_oracle.encode(d)
     assert np.array_equal(su, g["status"]) and np.array_equal(sd, g["status"])
     assert np.array_equal(vu, g["u_right"]) and np.array_equal(vd, g["depth"])
+
+
+# oracle_octree_ties of synthetic pair 0's left image (synth.make_pair(0)), per level: straddle, tie runs,
+# careful iterations, straddled run's nodes, of which divided (profiles/octree_ties.json has the workloads)
+TIES_PAIR0_LEFT = [[1, 10, 1, 13, 3], [1, 5, 1, 14, 13], [1, 4, 1, 8, 2], [1, 22, 2, 7, 4], [1, 14, 2, 8, 2],
+                   [1, 15, 2, 7, 4], [0, 10, 2, 0, 0], [1, 6, 3, 6, 1]]
+TIES_KITTI06 = [[1, 24, 1, 7, 2], [0, 19, 1, 0, 0], [0, 10, 1, 0, 0], [1, 7, 1, 5, 4], [0, 5, 1, 0, 0], [1, 13, 2, 6, 2],
+                [1, 14, 2, 5, 3], [1, 9, 2, 2, 1]]
+
+
+def test_octree_tie_report(kitti_png):
+    """SURVEY H1 / VERDICT r4 item 3: the tie report of the oracle, pinned, and shown to mean what it says by a
+    second admissible address order (the oldest of equal-size nodes divided first): on a level without a
+    straddle both orders keep the same keypoints (at most their order differs, and only where equal-size runs
+    were divided); on a straddled level the kept set may differ — it does on most of them."""
+    ex = O.OracleExtractor()
+    assert ex.octree_ties(kitti_png).tolist() == TIES_KITTI06
+    L = synth.make_pair(0)[0]
+    ties = ex.octree_ties(L)
+    assert ties.tolist() == TIES_PAIR0_LEFT
+    ex.extract(L)
+    n_per = ex.tables()["n_per_level"]
+    set_differs = []
+    for l, lvl in enumerate(ex.pyramid()):
+        h, w = lvl.shape
+        K = [tuple(r) for r in O.level_candidates(ex.p, lvl).tolist()]
+        a = _octree_py(K, 16, w - 16, 16, h - 16, int(n_per[l]))
+        b = _octree_py(K, 16, w - 16, 16, h - 16, int(n_per[l]), reverse_ties=True)
+        assert [tuple(r) for r in O.octree(np.array(K, np.int32), 16, w - 16, 16, h - 16, int(n_per[l])).tolist()] == a
+        if ties[l, 0] == 0:
+            assert sorted(a) == sorted(b), f"level {l}: no straddle reported, yet the kept keypoints differ"
+        else:
+            set_differs.append(sorted(a) != sorted(b))
+        if ties[l, 1] == 0:
+            assert a == b, f"level {l}: no tie run reported, yet the keypoint order differs"
+    assert sum(set_differs) > len(set_differs) // 2, set_differs

@@ -16,7 +16,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--handles", default="1,2,4", help="handle counts to try (pairs split by dist.shard)")
+    ap.add_argument("--graphs", default="0,1", help="graph settings to try")
+    ap.add_argument("--no-frame", action="store_true")
     a = ap.parse_args()
+    import os
+    from pyorbslam_amd.dist import shard
     import torch
     from pyorbslam_amd import synth
     from pyorbslam_amd._lib import call
@@ -25,15 +30,16 @@ def main():
     dev = torch.device("cuda", 0)
     out = {}
     imgs = torch.from_numpy(synth.make_batch(8, seed0=0)).to(dev)
-    for graphs in (False, True):
-        for handles in (1, 2, 4):
-            per = 8 // handles
-            fes = [StereoFrontEnd(max_pairs=per, lanes=1, graphs=graphs) for _ in range(handles)]
+    out["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
+    for graphs in [bool(int(v)) for v in a.graphs.split(",")]:
+        for handles in [int(v) for v in a.handles.split(",")]:
+            parts = [shard(8, handles, i) for i in range(handles)]
+            fes = [StereoFrontEnd(max_pairs=n, lanes=1, graphs=graphs) for _, n in parts]
             sts = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(handles - 1)]
 
             def step():
-                for i, (f, s) in enumerate(zip(fes, sts)):
-                    f.enqueue(imgs[2 * per * i: 2 * per * (i + 1)], per, stream_ptr=s.cuda_stream)
+                for (p0, n), f, s in zip(parts, fes, sts):
+                    f.enqueue(imgs[2 * p0: 2 * (p0 + n)], n, stream_ptr=s.cuda_stream)
             for _ in range(10):
                 step()
             torch.cuda.synchronize(dev)
@@ -55,7 +61,7 @@ def main():
                                                              "pairs_per_s": round(8 / ms * 1e3, 1)}
             del fes
     L, R = synth.make_pair(3)
-    for graphs in (False, True):
+    for graphs in (() if a.no_frame else (False, True)):
         ex, er = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
         call("orbfe_set_graphs", ex.handle, int(graphs))
         Lc, Rc = np.ascontiguousarray(L), np.ascontiguousarray(R)
