@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "orbfe_common.h"
 #include <type_traits>
@@ -1561,6 +1562,11 @@ constexpr int kObThreads = 256;
 #endif
 constexpr int kObBatch = ORBFE_OB_BATCH;    // slot loads in flight per thread in the first sweep
 constexpr uint32_t kObDeep = 0x80000000u;   // bin flag: holds nodes deeper than D0 (deep sweep / final map)
+// The node passes keep the list in wave 0's registers (kObNpl consecutive nodes per lane) when the level's
+// node capacity fits, i.e. max_ncap <= 64 kObNpl (every KITTI / EuRoC configuration up to ~3 900 features);
+// larger ones take the LDS-list passes (REG = false).
+constexpr int kObNpl = 8;
+__host__ __device__ inline bool octree_reg_passes(int max_ncap) { return max_ncap <= 64 * kObNpl; }
 
 // LDS ordering inside wave 0's node passes (the other waves wait at a workgroup barrier meanwhile)
 __device__ __forceinline__ void wsync() {
@@ -1601,6 +1607,46 @@ __device__ int wave_scan_lds(int* a, int n) {
 template <int S>
 __device__ __forceinline__ uint32_t dpp_shr(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x110 + S, 0xF, 0xF, false);
+}
+
+// Wave-wide inclusive scan (sum) with DPP row shifts and row broadcasts (no LDS, no bpermute); every lane
+// active.  Lane 63 holds the total.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ __forceinline__ int wave_total_dpp(int v) { return __builtin_amdgcn_readlane(wave_incl_scan_dpp(v), 63); }
+// wave maximum of non-negative values, in every lane
+__device__ __forceinline__ int wave_max_dpp(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+// Exclusive scan, in place, of a list held lane-major in registers (lane l holds elements l N .. l N + N - 1);
+// returns the total.
+template <int N>
+__device__ __forceinline__ int chunk_excl_scan(int (&v)[N]) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int x = v[k];
+        v[k] = s;
+        s += x;
+    }
+    const int inc = wave_incl_scan_dpp(s);
+    const int ex = inc - s;
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] += ex;
+    return __builtin_amdgcn_readlane(inc, 63);
 }
 
 // One key per lane, its bin b (0xFFFFFFFF: no key) and value v = response << 24 | 0xFFFFFF - index.  Lanes
@@ -1672,7 +1718,7 @@ __host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB
     take(10, 4 * (size_t)NC);
     take(11, 4 * (size_t)NC);
     take(12, 4 * (size_t)NC);
-    take(13, 8 * (size_t)NC);
+    take(13, 8 * (size_t)(NC > 64 * kObNpl ? NC : 64 * kObNpl));  // + the register passes' full-chunk reads
     take(14, 8 * (size_t)NC);
     take(15, 4 * (size_t)NC);
     take(16, (size_t)NC);
@@ -1684,7 +1730,7 @@ __host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB
 
 // NT threads: 256 (large batches: the workgroups of many images share the CUs) or 1 024 for small batches,
 // where one image's level-0 workgroup is the critical path and its key sweeps take 4x fewer rounds.
-template <int NT>
+template <int NT, bool REG>
 __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
                                                             const int* __restrict__ cell_count,
                                                             const uint32_t* __restrict__ slots,
@@ -1881,6 +1927,42 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             }
         });
     };
+    // REG: the current node list by position in LDS, packed (code | (count << 8 | depth) << 32), written by
+    // every pass of wave 0 and read back into its registers; the deep sweeps read it in place
+    uint64_t* lst = d.srt;
+    auto node_code = [&](int p) { return (uint32_t)lst[p]; };
+    auto node_dep = [&](int p) { return (int)((lst[p] >> 32) & 0xFFu); };
+    auto deep_sort_l = [&](int nn) {
+        for (int i = t; i < nn; i += NT) {
+            const int p = d.dl[i];
+            const uint32_t ci = node_code(p);
+            int r = 0;
+            for (int j = 0; j < nn; ++j) r += node_code(d.dl[j]) < ci;
+            d.sp[r] = (int)ci;
+            d.sd[r] = p;
+        }
+    };
+    auto deep_find_l = [&](int nn, uint32_t cd) {
+        int lo = 0, hi = nn - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((uint32_t)d.sp[mid] <= cd) lo = mid; else hi = mid - 1;
+        }
+        const int p = d.sd[lo];
+        return (uint32_t)d.sp[lo] <= cd && ((cd ^ node_code(p)) >> (2 * (D - node_dep(p)))) == 0u ? p : -1;
+    };
+    auto deep_sweep_l = [&](int nn) {
+        deep_sort_l(nn);
+        __syncthreads();
+        for_cached(t, NT, std::integral_constant<int, 1>{}, [&](int kk, uint32_t, uint32_t cd) {
+            if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
+            const int p = deep_find_l(nn, cd);
+            if (p >= 0) {
+                const int q = (int)((cd >> (2 * (D - node_dep(p) - 1))) & 3u);
+                atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
+            }
+        });
+    };
     // ---- 2. wave 0: cumulative counts, initial columns (:543-584), the passes (:585-737); the other waves
     //      wait for deep sweeps (s_cmd: 1 | list << 1 with s_nd nodes; 0 when the passes are over)
     if (t >= 64) {
@@ -1888,9 +1970,243 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             __syncthreads();  // a command (deep_counts) or the end of the passes
             const int cmd = s_cmd;
             if (cmd == 0) break;
-            deep_sweep(s_nd, cmd >> 1);
+            if constexpr (REG) deep_sweep_l(s_nd);
+            else deep_sweep(s_nd, cmd >> 1);
             __syncthreads();  // sweep complete
         }
+    } else if constexpr (REG) {
+        // ---------------- register-resident passes: lane l holds list positions l NP .. l NP + NP - 1; a pass
+        // computes every node's children counts (bin prefix sums, or the deep sweep's counts), the new
+        // positions by chunk scans, scatters the new list into LDS and reads it back
+        constexpr int NP = kObNpl, CAP = 64 * kObNpl;
+        wave_scan_lds((int*)d.bins, B);
+        if (t == 0) d.bins[B] = (uint32_t)K;
+        wsync();
+        auto cum = [&](int b) { return (int)(d.bins[b] & ~kObDeep); };
+        auto pack = [](uint32_t code, int n, int dp) {
+            return (uint64_t)code | ((uint64_t)(((uint32_t)n << 8) | (uint32_t)dp) << 32);
+        };
+        int S = 0;
+        bool ovf = false;
+        for (int i0 = 0; i0 < L.n_ini; i0 += 64) {  // empty columns removed, column order
+            const int i = i0 + t;
+            int n = 0;
+            if (i < L.n_ini) n = cum((i + 1) << (2 * D0)) - cum(i << (2 * D0));
+            const uint64_t bm = __ballot(n > 0);
+            if (n > 0) {
+                const int p = S + lanes_below(bm);
+                if (p < CAP) lst[p] = pack((uint32_t)i << (2 * D), n, 0);
+            }
+            S += __popcll(bm);
+        }
+        if (S > CAP) {  // cannot happen: kp_cap >= 4 nIni + 2 and the host picks REG only for kp_cap <= CAP
+            if (t == 0) atomicOr(overflow, 1);
+            S = CAP;
+        }
+        wsync();
+        // node k of this lane: code rc[k], count << 8 | depth in rh[k] (0 past the list's end)
+        uint32_t rc[NP], rh[NP];
+        auto load_list = [&](int n) {
+            const uint4* q = (const uint4*)(lst + t * NP);
+#pragma unroll
+            for (int k2 = 0; k2 < NP / 2; ++k2) {
+                const uint4 v = q[k2];
+                const bool a = t * NP + 2 * k2 < n, b = t * NP + 2 * k2 + 1 < n;
+                rc[2 * k2] = a ? v.x : 0u;
+                rh[2 * k2] = a ? v.y : 0u;
+                rc[2 * k2 + 1] = b ? v.z : 0u;
+                rh[2 * k2 + 1] = b ? v.w : 0u;
+            }
+        };
+        auto rn = [&](int k) { return (int)(rh[k] >> 8); };
+        auto rd = [&](int k) { return (int)(rh[k] & 0xFFu); };
+        load_list(S);
+        mark(2);
+        // the four children's key counts of the node at position e (registers code, count, depth)
+        auto child_counts = [&](uint32_t code, int dp, int e) {
+            int4 cc;
+            if (dp < D0) {
+                const int lo = (int)(code >> bsh), w = 1 << (2 * (D0 - dp - 1));
+                const int c0 = cum(lo), c1 = cum(lo + w), c2 = cum(lo + 2 * w), c3 = cum(lo + 3 * w), c4 = cum(lo + 4 * w);
+                cc = int4{c1 - c0, c2 - c1, c3 - c2, c4 - c3};
+            } else {
+                const uint32_t a = d.c4[2 * e], b = d.c4[2 * e + 1];
+                cc = int4{(int)(a & 0xFFFFu), (int)(a >> 16), (int)(b & 0xFFFFu), (int)(b >> 16)};
+            }
+            return cc;
+        };
+        auto nonempty = [](const int4& cc) { return (cc.x > 0) + (cc.y > 0) + (cc.z > 0) + (cc.w > 0); };
+        // children counts of the nodes deeper than D0 among the division candidates (cand[k]): one sweep of
+        // every wave over the cached keys
+        auto deep_counts = [&](const bool (&cand)[NP]) {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NP; ++k) any |= cand[k] && rd(k) >= D0;
+            if (!__ballot(any)) return;
+            int dk[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) dk[k] = cand[k] && rd(k) >= D0;
+            int o[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) o[k] = dk[k];
+            const int nd = chunk_excl_scan(o);
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (dk[k]) {
+                    const int e = t * NP + k;
+                    d.dl[o[k]] = e;
+                    d.c4[2 * e] = 0u;
+                    d.c4[2 * e + 1] = 0u;
+                    atomicOr(&d.bins[rc[k] >> bsh], kObDeep);
+                }
+            if (t == 0) {
+                s_cmd = 1;
+                s_nd = nd;
+            }
+            __syncthreads();  // the other waves start the sweep
+            deep_sweep_l(nd);
+            __syncthreads();  // every wave's counts are in
+            for (int i = t; i < nd; i += 64) atomicAnd(&d.bins[node_code(d.dl[i]) >> bsh], ~kObDeep);
+            wsync();
+        };
+        int C = 0, phase = 0;
+        bool done = false;
+        for (int iter = 0; !done; ++iter) {
+            if (iter > 4 * CAP + 64) {  // cannot happen (each pass grows the list or finishes); never hang
+                if (t == 0) atomicOr(overflow, 2);
+                break;
+            }
+            mark(8 + 4 * iter);
+            int nck[NP], kep[NP];
+            bool div[NP];
+            int Cn, Kk, nexp = 0;
+            int cbase[NP];
+            if (phase == 0) {
+                // ---------------- full pass (:605-664): divide every node holding more than one key
+#pragma unroll
+                for (int k = 0; k < NP; ++k) div[k] = t * NP + k < S && rn(k) > 1;
+                deep_counts(div);
+                int ne = 0;
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    const int4 cc = div[k] ? child_counts(rc[k], rd(k), t * NP + k) : int4{0, 0, 0, 0};
+                    nck[k] = nonempty(cc);
+                    ne += (cc.x > 1) + (cc.y > 1) + (cc.z > 1) + (cc.w > 1);
+                    kep[k] = t * NP + k < S && rn(k) == 1;
+                    cbase[k] = nck[k];
+                }
+                Cn = chunk_excl_scan(cbase);
+                Kk = chunk_excl_scan(kep);
+                nexp = wave_total_dpp(ne);
+            } else {
+                // ---------------- careful phase (:675-736): the expandable nodes of the last step (its
+                // children, positions < C) by size descending, equal sizes in creation order descending
+                // (= position ascending); divided until the list reaches N.  Sizes are taken group by group
+                // (wave maximum of the remaining sizes), a group in position order.
+                bool cand[NP];
+                int rem[NP];
+#pragma unroll
+                for (int k = 0; k < NP; ++k) cand[k] = t * NP + k < C && rn(k) > 1;
+                deep_counts(cand);
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    nck[k] = cand[k] ? nonempty(child_counts(rc[k], rd(k), t * NP + k)) : 0;
+                    rem[k] = cand[k] ? rn(k) : 0;
+                    div[k] = false;
+                    cbase[k] = 0;
+                }
+                int Scur = S, Cacc = 0;
+                for (;;) {
+                    int m = 0;
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) m = max(m, rem[k]);
+                    const int v = wave_max_dpp(m);
+                    if (v == 0) break;
+                    int x[NP], y[NP];
+                    int gl = 0;
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) {
+                        const bool gk = rem[k] == v;
+                        x[k] = gk ? nck[k] : 0;
+                        y[k] = gk ? nck[k] - 1 : 0;
+                        gl += gk;
+                    }
+                    chunk_excl_scan(x);
+                    chunk_excl_scan(y);
+                    int pl = 0, grow = 0, ch = 0;
+#pragma unroll
+                    for (int k = 0; k < NP; ++k)
+                        if (rem[k] == v) {
+                            if (Scur + y[k] < N) {  // the list before it is below N: divided (:729-730)
+                                div[k] = true;
+                                cbase[k] = Cacc + x[k];
+                                ++pl;
+                                grow += nck[k] - 1;
+                                ch += nck[k];
+                            }
+                            rem[k] = 0;
+                        }
+                    const int np = wave_total_dpp(pl), ng = wave_total_dpp(gl);
+                    Scur += wave_total_dpp(grow);
+                    Cacc += wave_total_dpp(ch);
+                    if (np < ng || Scur >= N) break;
+                }
+                Cn = Cacc;
+#pragma unroll
+                for (int k = 0; k < NP; ++k) kep[k] = t * NP + k < S && !div[k];
+                Kk = chunk_excl_scan(kep);
+            }
+            const int Sn = Cn + Kk;
+            if (Sn > CAP) {
+                ovf = true;
+                done = true;
+            } else {
+                // scatter: children in reverse creation order at the front (push_front, :620-659 / :690-725),
+                // the nodes not divided behind them in list order
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    if (div[k]) {  // the children counts again (LDS reads) rather than 4 NP more registers
+                        int c = cbase[k];
+                        const int dp = rd(k);
+                        const uint32_t code = rc[k];
+                        const int4 cc = child_counts(code, dp, t * NP + k);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int n = q == 0 ? cc.x : q == 1 ? cc.y : q == 2 ? cc.z : cc.w;
+                            if (n > 0) lst[Cn - 1 - c++] = pack(code | ((uint32_t)q << (2 * (D - dp - 1))), n, dp + 1);
+                        }
+                    } else if (t * NP + k < S) {
+                        lst[Cn + kep[k]] = (uint64_t)rc[k] | ((uint64_t)rh[k] << 32);
+                    }
+                }
+                wsync();
+                load_list(Sn);
+                if (phase == 0) {
+                    if (Sn >= N || Sn == S) done = true;              // :668-671
+                    else if (Sn + 3 * nexp > N) phase = 1;            // :672
+                } else if (Sn >= N || Sn == S) {
+                    done = true;                                      // :733-734
+                }
+                S = Sn;
+                C = Cn;
+            }
+        }
+        if (__ballot(ovf) && t == 0) atomicOr(overflow, 4);
+        // nodes deeper than D0 of the final list, for the final map
+        int o[NP], dk[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) o[k] = dk[k] = t * NP + k < S && rd(k) > D0;
+        const int nd = chunk_excl_scan(o);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (dk[k]) d.dl[o[k]] = t * NP + k;
+        if (t == 0) {
+            s_S = S;
+            s_cur = 0;
+            s_cmd = 0;
+        }
+        __syncthreads();  // the other waves leave their command loop
+        if (t == 0) s_nd = nd;
     } else {
         wave_scan_lds((int*)d.bins, B);
         if (t == 0) d.bins[B] = (uint32_t)K;
@@ -2182,11 +2498,13 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     const int S = s_S, nd = s_nd;
     const uint32_t* code = s_cur ? d.code1 : d.code0;
     const uint8_t* dep = s_cur ? d.dep1 : d.dep0;
+    auto fcode = [&](int p) { return REG ? node_code(p) : code[p]; };
+    auto fdep = [&](int p) { return REG ? node_dep(p) : (int)dep[p]; };
     uint32_t* best = (uint32_t*)d.sa;
     // a node of depth <= D0 covers whole bins: its best key is the maximum of their maxima
     for (int p = t; p < S; p += NT) {
-        const int dp = dep[p];
-        const int lo = (int)(code[p] >> bsh);
+        const int dp = fdep(p);
+        const int lo = (int)(fcode(p) >> bsh);
         uint32_t m = 0u;
         if (dp <= D0) {
             const int w = 1 << (2 * (D0 - dp));
@@ -2197,15 +2515,16 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     __syncthreads();
     // nodes deeper than D0: a sweep over the keys of their bins (bin flag, then the sorted deep nodes)
     if (nd > 0) {
-        for (int i = t; i < nd; i += NT) d.bins[code[d.dl[i]] >> bsh] = kObDeep;
+        for (int i = t; i < nd; i += NT) d.bins[fcode(d.dl[i]) >> bsh] = kObDeep;
         __syncthreads();
     }
     if (nd > 0) {
-        deep_sort(nd, code);
+        if constexpr (REG) deep_sort_l(nd);
+        else deep_sort(nd, code);
         __syncthreads();
         for_cached(t, NT, std::integral_constant<int, 2>{}, [&](int kk, uint32_t v, uint32_t cd) {
             if (kk >= K || d.bins[cd >> bsh] != kObDeep) return;
-            const int q = deep_find(nd, code, dep, cd);
+            const int q = REG ? deep_find_l(nd, cd) : deep_find(nd, code, dep, cd);
             if (q >= 0) atomicMax(&best[q], (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)kk));
         });
     }
@@ -3242,8 +3561,17 @@ size_t octree_bins_lds_bytes(const Geo& g, int maxcell) {
 // (a process with handles on two GPUs must raise them on each).
 constexpr int kMaxDevices = 64;
 struct LdsAttr {
-    int octree[3] = {64 * 1024, 64 * 1024, 64 * 1024};  // k_octree_bins<256>, k_octree, k_octree_bins<1024>
-    int cascade = 64 * 1024;                            // k_resize_cascade
+    std::vector<std::pair<const void*, int>> raised;  // kernel -> dynamic LDS limit raised on this device
+    int get(const void* fn) const {
+        for (const auto& e : raised)
+            if (e.first == fn) return e.second;
+        return 64 * 1024;
+    }
+    void set(const void* fn, int v) {
+        for (auto& e : raised)
+            if (e.first == fn) { e.second = v; return; }
+        raised.emplace_back(fn, v);
+    }
 };
 static LdsAttr g_lds[kMaxDevices];
 static std::mutex g_lds_mu;
@@ -3254,45 +3582,48 @@ static LdsAttr* lds_attr() {
     return &g_lds[dev];
 }
 
-hipError_t prepare_resize_cascade(int lds_bytes) {
+static hipError_t raise_lds(const void* fn, int bytes) {
     std::lock_guard<std::mutex> lk(g_lds_mu);
     LdsAttr* a = lds_attr();
     if (!a) return hipErrorInvalidDevice;
-    if (lds_bytes <= a->cascade) return hipSuccess;
-    if (lds_bytes > 160 * 1024) return hipErrorInvalidValue;
-    const hipError_t e =
-        hipFuncSetAttribute((const void*)k_resize_cascade, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    if (e == hipSuccess) a->cascade = lds_bytes;
+    if (bytes <= a->get(fn)) return hipSuccess;
+    if (bytes > 160 * 1024) return hipErrorInvalidValue;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) a->set(fn, bytes);
     return e;
 }
 
-hipError_t prepare_octree(const Geo& g, int maxcell) {
-    const size_t need[3] = {octree_bins_lds_bytes(g, maxcell), octree_lds_bytes(g, maxcell), octree_bins_lds_bytes(g, maxcell)};
-    const void* fn[3] = {(const void*)k_octree_bins<kObThreads>, (const void*)k_octree, (const void*)k_octree_bins<1024>};
-    std::lock_guard<std::mutex> lk(g_lds_mu);
-    LdsAttr* a = lds_attr();
-    if (!a) return hipErrorInvalidDevice;
-    for (int k = 0; k < 3; ++k) {
-        if ((int)need[k] <= a->octree[k] || need[k] > 160 * 1024) continue;
-        const hipError_t e = hipFuncSetAttribute(fn[k], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[k]);
-        if (e != hipSuccess) return e;
-        a->octree[k] = (int)need[k];
-    }
-    return hipSuccess;
-}
-
-// the limit raised on the current device for kernel k (0..2 octree, 3 cascade)
-static int lds_limit(int k) {
+// the limit raised on the current device for kernel fn
+static int lds_limit(const void* fn) {
     std::lock_guard<std::mutex> lk(g_lds_mu);
     const LdsAttr* a = lds_attr();
-    return !a ? 0 : k < 3 ? a->octree[k] : a->cascade;
+    return a ? a->get(fn) : 0;
+}
+
+hipError_t prepare_resize_cascade(int lds_bytes) { return raise_lds((const void*)k_resize_cascade, lds_bytes); }
+
+static const void* octree_bins_fn(const Geo& g, bool wide) {
+    const bool reg = octree_reg_passes(g.max_ncap);
+    return wide ? (reg ? (const void*)k_octree_bins<1024, true> : (const void*)k_octree_bins<1024, false>)
+                : (reg ? (const void*)k_octree_bins<kObThreads, true> : (const void*)k_octree_bins<kObThreads, false>);
+}
+
+hipError_t prepare_octree(const Geo& g, int maxcell) {
+    const size_t nb = octree_bins_lds_bytes(g, maxcell), no = octree_lds_bytes(g, maxcell);
+    hipError_t e = hipSuccess;
+    if (nb <= 160 * 1024) {
+        if ((e = raise_lds(octree_bins_fn(g, false), (int)nb)) != hipSuccess) return e;
+        if ((e = raise_lds(octree_bins_fn(g, true), (int)nb)) != hipSuccess) return e;
+    }
+    if (no <= 160 * 1024) e = raise_lds((const void*)k_octree, (int)no);
+    return e;
 }
 
 hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                                  const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
                                  int lds_bytes, int n_images, hipStream_t s, int* zero_word) {
     if (g.nlevels < 2 || n_images <= 0) return hipSuccess;
-    if (lds_bytes > lds_limit(3)) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
+    if (lds_bytes > lds_limit((const void*)k_resize_cascade)) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
     hipLaunchKernelGGL(k_resize_cascade, dim3(n_strips, n_images), dim3(512), (size_t)lds_bytes, s, g, in, in_pitch, ws,
                        xt, yt, strips, off_b, off_x, zero_word);
     return hipGetLastError();
@@ -3303,19 +3634,19 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
     if (g.oct_v == 0) {
         const size_t lds = octree_bins_lds_bytes(g, maxcell);
-        if ((int)lds > lds_limit(0) || (int)lds > lds_limit(2)) return hipErrorInvalidConfiguration;  // prepare_octree
         // 1 024 threads for small batches (variant 1 / 2 force 256 / 1 024, tools/microbench.py)
         const bool wide = variant == 2 || (variant != 1 && n_images < kSmallBatchImages);
-        if (wide)
-            hipLaunchKernelGGL(k_octree_bins<1024>, dim3(n_images, g.nlevels), dim3(1024), lds, s, g, cells, cell_count,
-                               slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
-        else
-            hipLaunchKernelGGL(k_octree_bins<kObThreads>, dim3(n_images, g.nlevels), dim3(kObThreads), lds, s, g, cells,
-                               cell_count, slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
+        const void* fn = octree_bins_fn(g, wide);
+        if ((int)lds > lds_limit(fn)) return hipErrorInvalidConfiguration;  // prepare_octree
+        const bool reg = octree_reg_passes(g.max_ncap);
+        auto k = wide ? (reg ? k_octree_bins<1024, true> : k_octree_bins<1024, false>)
+                      : (reg ? k_octree_bins<kObThreads, true> : k_octree_bins<kObThreads, false>);
+        hipLaunchKernelGGL(k, dim3(n_images, g.nlevels), dim3(wide ? 1024 : kObThreads), lds, s, g, cells, cell_count,
+                           slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
         return hipGetLastError();
     }
     const size_t lds = octree_lds_bytes(g, maxcell);
-    if ((int)lds > lds_limit(1)) return hipErrorInvalidConfiguration;
+    if ((int)lds > lds_limit((const void*)k_octree)) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL(k_octree, dim3(n_images, g.nlevels), dim3(kOctThreads), lds, s, g, cells, cell_count, slots, kd, kn,
                        lvl_kp, lvl_count, overflow, maxcell, variant, prof);
     return hipGetLastError();

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--graphs", type=int, default=1)
     ap.add_argument("--frame", action="store_true")
+    ap.add_argument("--handles", type=int, default=1, help="the pairs split over this many handles / streams")
     ap.add_argument("--pyramid", type=int, default=0, help="--frame: want_pyramid (the sheared views too)")
     a = ap.parse_args()
     import torch
@@ -34,9 +35,13 @@ def main():
                  float(np.float32(KITTI_FX)), a.pyramid)
         return
     imgs = torch.from_numpy(synth.make_batch(a.pairs, seed0=0)).cuda()
-    fe = StereoFrontEnd(max_pairs=a.pairs, lanes=1, graphs=bool(a.graphs))
+    from pyorbslam_amd.dist import shard
+    parts = [shard(a.pairs, a.handles, i) for i in range(a.handles)]
+    fes = [StereoFrontEnd(max_pairs=n, lanes=1, graphs=bool(a.graphs)) for _, n in parts]
+    sts = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(a.handles - 1)]
     for _ in range(5 + a.steps):
-        fe.enqueue(imgs, a.pairs)
+        for (p0, n), fe, st in zip(parts, fes, sts):
+            fe.enqueue(imgs[2 * p0: 2 * (p0 + n)], n, stream_ptr=st.cuda_stream)
     torch.cuda.synchronize()
 
 
