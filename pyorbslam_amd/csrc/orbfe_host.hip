@@ -731,8 +731,10 @@ void prepare_pyramid(orbfe_ctx& c, int n) {
 // zero_ovf: the batch's overflow word is cleared by the first pyramid launch instead of a separate memset
 // (one stream operation less in front of the chain); only for an enqueue that owns the word alone (not the
 // concurrent chunks of orbfe_set_lanes, one of which could clear a bound another chunk already flagged).
+// bucket: the stereo arguments of the range's pairs (n / 2 of them) when k_orb's launch is to build their row
+// buckets too (the front-end enqueues; orb_fuses_bucket)
 void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int n, hipStream_t s, bool prof,
-                   int lane = -1, bool zero_ovf = false) {
+                   int lane = -1, bool zero_ovf = false, const StereoArgs* bucket = nullptr) {
     const Geo& g = c.geo;
     const uint8_t* in = d_in + (int64_t)i0 * pitch;
     uint8_t* ws = c.d_ws.p + (int64_t)i0 * g.ws_bytes;
@@ -765,7 +767,7 @@ void extract_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int i0, int
     HIPCK(launch_octree(g, c.d_cells.p, cell_count, slots, c.d_octab.p, kd, kn, lvl_kp, lvl_count, c.d_overflow.p,
                         c.maxcell, n, s));
     if (prof) prof_mark(c, s, 3);
-    HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s));
+    HIPCK(launch_orb(g, in, pitch, ws, lvl_kp, lvl_count, kps, desc, count, n, c.d_orb.p, s, 0, bucket, bucket ? n / 2 : 0));
     if (prof) prof_mark(c, s, 4);
 }
 
@@ -801,9 +803,8 @@ void stereo_consts(double bf, float fx, StereoArgs& a) {
     a.bf = bf;
 }
 
-// Pairs [p0, p0 + n) (images 2p, 2p + 1) of the extracted batch at d_in.
-void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int n, double bf, float fx,
-                  hipStream_t s) {
+// Stereo arguments of pairs [p0, ...) (images 2p, 2p + 1) of the batch at d_in.
+StereoArgs stereo_args(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, double bf, float fx) {
     const Geo& g = c.geo;
     const int64_t i0 = 2 * (int64_t)p0;
     StereoArgs a{};
@@ -826,9 +827,20 @@ void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int 
     a.status = c.d_status.p + (int64_t)p0 * g.kp_cap;
     a.match_r = c.d_match.p + (int64_t)p0 * g.kp_cap;
     a.out_stride = g.kp_cap;
+    a.lkpR = c.d_lvl_kp.p + (i0 + 1) * g.lvl_kp_cap;
+    a.lkp_stride = 2 * (int64_t)g.lvl_kp_cap;
+    a.lcntR = c.d_lvl_count.p + (i0 + 1) * g.nlevels;
+    a.lcnt_stride = 2 * (int64_t)g.nlevels;
     stereo_buffers(c, a, p0);
     stereo_consts(bf, fx, a);
-    HIPCK(launch_stereo(g, a, n, s));
+    return a;
+}
+
+// Pairs [p0, p0 + n) of the extracted batch at d_in; buckets_built: extract_range's k_orb launch built them.
+void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int n, double bf, float fx,
+                  hipStream_t s, bool buckets_built = false) {
+    const StereoArgs a = stereo_args(c, d_in, pitch, p0, bf, fx);
+    HIPCK(launch_stereo(c.geo, a, n, s, buckets_built));
 }
 
 // Marks the end of a batch enqueue on s: orbfe_batch_pack_device orders its k_pack after it, whatever
@@ -916,8 +928,10 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
         prepare_pyramid(c, 2 * n_pairs);
         run_enqueue(c, ORBFE_GRAPH_BATCH, {1, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx)}, s,
                     [&](hipStream_t q) {
-                        extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true, -1, true);
-                        stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, q);
+                        const bool fuse = orb_fuses_bucket(c.geo);
+                        const StereoArgs sa = stereo_args(c, d_in, pitch, 0, bf, fx);
+                        extract_range(c, d_in, pitch, 0, 2 * n_pairs, q, true, -1, true, fuse ? &sa : nullptr);
+                        stereo_range(c, d_in, pitch, 0, n_pairs, bf, fx, q, fuse);
                         prof_mark(c, q, 5);
                     });
     } else {
@@ -935,8 +949,10 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             prepare_pyramid(c, 2 * (p1 - p0));
             hipStream_t ls = c.lane_stream[k];
             HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
-            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k);
-            stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls);
+            const bool fuse = orb_fuses_bucket(c.geo);
+            const StereoArgs sa = stereo_args(c, d_in, pitch, p0, bf, fx);
+            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k, false, fuse ? &sa : nullptr);
+            stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls, fuse);
             if (k == 0) prof_mark(c, ls, 5);
             HIPCK(hipEventRecord(c.lane_done[k], ls));
         }
@@ -1135,8 +1151,10 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
         prepare_pyramid(*h, 2);
         run_enqueue(*h, ORBFE_GRAPH_FRAME, key, s, [&](hipStream_t q) {
             HIPCK(hipMemcpyAsync(h->d_in.p, h->h_in.p, (size_t)pitch + (size_t)width * height, hipMemcpyHostToDevice, q));
-            extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, -1, true);
-            stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q);
+            const bool fuse = orb_fuses_bucket(g);
+            const StereoArgs sa = stereo_args(*h, h->d_in.p, pitch, 0, bf, fx);
+            extract_range(*h, h->d_in.p, pitch, 0, 2, q, false, -1, true, fuse ? &sa : nullptr);
+            stereo_range(*h, h->d_in.p, pitch, 0, 1, bf, fx, q, fuse);
             if (want_pyramid) HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p, h->d_shear.p, 2, q));
             // every result into the page-locked frame buffer with ONE kernel's stores over PCIe (k_copy_segments;
             // 8-9 copy-engine transfers cost ~60 us per frame in fixed costs, rocprof round 4)
@@ -1270,6 +1288,8 @@ int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, fl
         a.status = hl->d_status.p;
         a.match_r = hl->d_match.p;
         a.out_stride = g.kp_cap;
+        a.lkpR = hr->d_lvl_kp.p;
+        a.lcntR = hr->d_lvl_count.p;
         stereo_buffers(*hl, a, 0);
         a.kp_stride = 0;
         stereo_consts(bf, fx, a);

@@ -35,6 +35,12 @@ struct StereoArgs {
     uint16_t* bucket_idx;
     int64_t bucket_cap;
     float2* rinfo;
+    // the right images' level keypoints / counts (octree output) the buckets are built from, and their strides
+    // between consecutive pairs
+    const uint32_t* lkpR;
+    int64_t lkp_stride;
+    const int* lcntR;
+    int64_t lcnt_stride;
     float maxD;               // np.float32(bf / np.float32(bf / fx32))   (Frame.py:43, 181-183)
     float bf32;               // np.float32(bf): what `mbf / disparity` promotes bf to
     double bf;
@@ -99,12 +105,17 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          const uint32_t* octab, uint32_t* kd, uint16_t* kn, uint32_t* lvl_kp, int* lvl_count, int* overflow,
                          int maxcell, int n_images, hipStream_t s, int variant = 0, long long* prof = nullptr);
 // fused IC angle + 7x7 blur of each keypoint's neighbourhood + steered BRIEF (replaces k_blur + k_describe)
+// bucket (optional): the stereo row buckets of pairs 0 .. n_bucket - 1 are built by extra workgroups of the
+// same launch (they need the octree's level keypoints only); only when orb_fuses_bucket(g)
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
-                      const uint32_t* tab, hipStream_t s, int variant = 0);
+                      const uint32_t* tab, hipStream_t s, int variant = 0, const StereoArgs* bucket = nullptr,
+                      int n_bucket = 0);
+bool orb_fuses_bucket(const Geo& g);
 // k_orb's item table (orb_tables on the host): 192 horizontal items + 256 centroid slots x 4 dwords
 constexpr int kOrbTabWords = 192 + 256 * 4;
-hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s);
+// buckets_built: k_orb's launch already built the row buckets (launch_orb's bucket argument)
+hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s, bool buckets_built = false);
 // sheared views of every level (GetImagePyramid), out: n_images x g.shear_bytes
 hipError_t launch_shear(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, uint8_t* out, int n_images,
                         hipStream_t s);

@@ -1696,6 +1696,7 @@ struct ObLds {
     uint32_t* tab;         // the level's X then Y table
     uint32_t* bmax;        // per bin: max of (response << 24 | 0xFFFFFF - key index)
     uint16_t* bcell;       // per 64-key block: the cell of its first key (the first oct_kblk_max blocks)
+    uint64_t* lst2;        // FLAT: the second node list (packed code | (count << 8 | depth) << 32)
 };
 
 __host__ __device__ inline size_t ob_align(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -1725,12 +1726,13 @@ __host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB
     take(17, 4 * (size_t)TW);
     take(18, 4 * (size_t)B);
     take(19, 2 * (size_t)KB);
+    take(20, 8 * (size_t)(NC <= 64 * kObNpl ? 64 * kObNpl : 0));  // the flat passes' second list buffer
     return o;
 }
 
 // NT threads: 256 (large batches: the workgroups of many images share the CUs) or 1 024 for small batches,
 // where one image's level-0 workgroup is the critical path and its key sweeps take 4x fewer rounds.
-template <int NT, bool REG>
+template <int NT, bool FLAT>
 __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
                                                             const int* __restrict__ cell_count,
                                                             const uint32_t* __restrict__ slots,
@@ -1772,7 +1774,8 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             case 16: d.proc = p; break;
             case 17: d.tab = (uint32_t*)p; break;
             case 18: d.bmax = (uint32_t*)p; break;
-            default: d.bcell = (uint16_t*)p; break;
+            case 19: d.bcell = (uint16_t*)p; break;
+            default: d.lst2 = (uint64_t*)p; break;
         }
     });
     const int N = L.n_feat, ncell = L.ncell;
@@ -1927,286 +1930,465 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             }
         });
     };
-    // REG: the current node list by position in LDS, packed (code | (count << 8 | depth) << 32), written by
-    // every pass of wave 0 and read back into its registers; the deep sweeps read it in place
+    // FLAT: node lists by position in LDS, packed (code | (count << 8 | depth) << 32); the deep sweeps read
+    // the current one in place
     uint64_t* lst = d.srt;
-    auto node_code = [&](int p) { return (uint32_t)lst[p]; };
-    auto node_dep = [&](int p) { return (int)((lst[p] >> 32) & 0xFFu); };
-    auto deep_sort_l = [&](int nn) {
+    auto node_code = [](const uint64_t* l, int p) { return (uint32_t)l[p]; };
+    auto node_cnt = [](const uint64_t* l, int p) { return (int)(l[p] >> 40); };
+    auto node_dep = [](const uint64_t* l, int p) { return (int)((l[p] >> 32) & 0xFFu); };
+    auto deep_sort_l = [&](int nn, const uint64_t* l) {
         for (int i = t; i < nn; i += NT) {
             const int p = d.dl[i];
-            const uint32_t ci = node_code(p);
+            const uint32_t ci = node_code(l, p);
             int r = 0;
-            for (int j = 0; j < nn; ++j) r += node_code(d.dl[j]) < ci;
+            for (int j = 0; j < nn; ++j) r += node_code(l, d.dl[j]) < ci;
             d.sp[r] = (int)ci;
             d.sd[r] = p;
         }
     };
-    auto deep_find_l = [&](int nn, uint32_t cd) {
+    auto deep_find_l = [&](int nn, uint32_t cd, const uint64_t* l) {
         int lo = 0, hi = nn - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if ((uint32_t)d.sp[mid] <= cd) lo = mid; else hi = mid - 1;
         }
         const int p = d.sd[lo];
-        return (uint32_t)d.sp[lo] <= cd && ((cd ^ node_code(p)) >> (2 * (D - node_dep(p)))) == 0u ? p : -1;
-    };
-    auto deep_sweep_l = [&](int nn) {
-        deep_sort_l(nn);
-        __syncthreads();
-        for_cached(t, NT, std::integral_constant<int, 1>{}, [&](int kk, uint32_t, uint32_t cd) {
-            if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
-            const int p = deep_find_l(nn, cd);
-            if (p >= 0) {
-                const int q = (int)((cd >> (2 * (D - node_dep(p) - 1))) & 3u);
-                atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
-            }
-        });
+        return (uint32_t)d.sp[lo] <= cd && ((cd ^ node_code(l, p)) >> (2 * (D - node_dep(l, p)))) == 0u ? p : -1;
     };
     // ---- 2. wave 0: cumulative counts, initial columns (:543-584), the passes (:585-737); the other waves
     //      wait for deep sweeps (s_cmd: 1 | list << 1 with s_nd nodes; 0 when the passes are over)
-    if (t >= 64) {
-        for (;;) {
-            __syncthreads();  // a command (deep_counts) or the end of the passes
-            const int cmd = s_cmd;
-            if (cmd == 0) break;
-            if constexpr (REG) deep_sweep_l(s_nd);
-            else deep_sweep(s_nd, cmd >> 1);
-            __syncthreads();  // sweep complete
-        }
-    } else if constexpr (REG) {
-        // ---------------- register-resident passes: lane l holds list positions l NP .. l NP + NP - 1; a pass
-        // computes every node's children counts (bin prefix sums, or the deep sweep's counts), the new
-        // positions by chunk scans, scatters the new list into LDS and reads it back
-        constexpr int NP = kObNpl, CAP = 64 * kObNpl;
-        wave_scan_lds((int*)d.bins, B);
-        if (t == 0) d.bins[B] = (uint32_t)K;
-        wsync();
-        auto cum = [&](int b) { return (int)(d.bins[b] & ~kObDeep); };
+    if constexpr (FLAT) {
+        // ---------------- all threads (FLAT).  The full passes (:593-671) in closed form from the bin
+        // histogram: after pass j the list is the depth-j nodes created in pass j (every nonempty child of a
+        // node holding >= 2 keys) in reverse creation order, then the single-key nodes created in passes
+        // j-1, ..., 0, each group in its own reverse creation order (push_front keeps them in place).
+        // Creation order alternates direction from depth to depth, so every group's list order is the
+        // numeric order of the node's Morton index with every other 2-bit digit (and, at odd depths, the
+        // column) mirrored: the list is one flat enumeration + one block scan.  The careful phase
+        // (:675-737) divides candidates in (size desc, creation desc) order: a stable radix sort of the
+        // candidates by size, a scan of the list growth in that order for the break, scans for the
+        // positions.  Nodes deeper than D0 take the deep sweeps (every thread).
+        constexpr int CAPL = 64 * kObNpl;
+        constexpr int LP = (CAPL + NT - 1) / NT;      // list positions per thread (p = t LP + k)
+        constexpr int EB = (2048 + 1 + NT - 1) / NT;  // bins (+ the total) per thread
+        constexpr int EP = (2816 + NT - 1) / NT;      // closed-form enumeration: sum over depths <= D0 of nodes
+        constexpr int NW = NT / 64;
+        __shared__ int s_red[NW];
+        __shared__ int s_dc[3][16];                    // per depth: listed nodes, of which single-key, >= 2 keys
+        __shared__ int s_cw[NW][16];                   // radix: per-wave digit counts
+        __shared__ int s_co[NW][16];                   // radix: per-wave digit offsets
+        __shared__ int s_m[4];
+        const int lane = t & 63, wv = t >> 6;
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        // exclusive block scan of v (thread-contiguous order t * E + k), in place; returns the total
+        auto bscan = [&](auto& v) -> int {
+            constexpr int E = sizeof(v) / sizeof(v[0]);
+            int s0 = 0;
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                const int x = v[k];
+                v[k] = s0;
+                s0 += x;
+            }
+            const int inc = wave_incl_scan_dpp(s0);
+            if (lane == 63) s_red[wv] = inc;
+            __syncthreads();
+            int off = 0, tot = 0;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int r = s_red[i];
+                off += i < wv ? r : 0;
+                tot += r;
+            }
+            const int ex = off + inc - s0;
+#pragma unroll
+            for (int k = 0; k < E; ++k) v[k] += ex;
+            __syncthreads();
+            return tot;
+        };
         auto pack = [](uint32_t code, int n, int dp) {
             return (uint64_t)code | ((uint64_t)(((uint32_t)n << 8) | (uint32_t)dp) << 32);
         };
-        int S = 0;
-        bool ovf = false;
-        for (int i0 = 0; i0 < L.n_ini; i0 += 64) {  // empty columns removed, column order
-            const int i = i0 + t;
-            int n = 0;
-            if (i < L.n_ini) n = cum((i + 1) << (2 * D0)) - cum(i << (2 * D0));
-            const uint64_t bm = __ballot(n > 0);
-            if (n > 0) {
-                const int p = S + lanes_below(bm);
-                if (p < CAP) lst[p] = pack((uint32_t)i << (2 * D), n, 0);
-            }
-            S += __popcll(bm);
-        }
-        if (S > CAP) {  // cannot happen: kp_cap >= 4 nIni + 2 and the host picks REG only for kp_cap <= CAP
-            if (t == 0) atomicOr(overflow, 1);
-            S = CAP;
-        }
-        wsync();
-        // node k of this lane: code rc[k], count << 8 | depth in rh[k] (0 past the list's end)
-        uint32_t rc[NP], rh[NP];
-        auto load_list = [&](int n) {
-            const uint4* q = (const uint4*)(lst + t * NP);
+        for (int i = t; i < NC; i += NT) d.proc[i] = 0;  // (ordered before use by bscan's barriers)
+        // cumulative bin counts, bins[B] = K
+        {
+            int v[EB];
 #pragma unroll
-            for (int k2 = 0; k2 < NP / 2; ++k2) {
-                const uint4 v = q[k2];
-                const bool a = t * NP + 2 * k2 < n, b = t * NP + 2 * k2 + 1 < n;
-                rc[2 * k2] = a ? v.x : 0u;
-                rh[2 * k2] = a ? v.y : 0u;
-                rc[2 * k2 + 1] = b ? v.z : 0u;
-                rh[2 * k2 + 1] = b ? v.w : 0u;
+            for (int k = 0; k < EB; ++k) {
+                const int i = t * EB + k;
+                v[k] = i < B ? (int)d.bins[i] : 0;
             }
+            bscan(v);
+#pragma unroll
+            for (int k = 0; k < EB; ++k)
+                if (t * EB + k <= B) d.bins[t * EB + k] = (uint32_t)v[k];
+            if (t < 48) (&s_dc[0][0])[t] = 0;
+            __syncthreads();
+        }
+        auto cum = [&](int b) { return (int)(d.bins[b] & ~kObDeep); };
+        auto ncnt = [&](int dd, int i) {
+            const int sh = 2 * (D0 - dd);
+            return cum((i + 1) << sh) - cum(i << sh);
         };
-        auto rn = [&](int k) { return (int)(rh[k] >> 8); };
-        auto rd = [&](int k) { return (int)(rh[k] & 0xFFu); };
-        load_list(S);
+        // per depth d <= D0: nodes a pass creates (nonempty, parent holds >= 2 keys; every nonempty column at
+        // depth 0), how many of them hold one key, how many >= 2
+        for (int dd = 0; dd <= D0; ++dd) {
+            const int P = L.n_ini << (2 * dd);
+            for (int i0 = 0; i0 < P; i0 += NT) {
+                const int i = i0 + t;
+                int c = 0, pc = 2;
+                if (i < P) {
+                    c = ncnt(dd, i);
+                    if (dd) pc = ncnt(dd - 1, i >> 2);
+                }
+                const bool q = i < P && c >= 1 && pc >= 2;
+                const uint64_t ba = __ballot(q), b1 = __ballot(q && c == 1), bx = __ballot(q && c >= 2);
+                if (lane == 0 && ba) {
+                    atomicAdd(&s_dc[0][dd], __popcll(ba));
+                    atomicAdd(&s_dc[1][dd], __popcll(b1));
+                    atomicAdd(&s_dc[2][dd], __popcll(bx));
+                }
+            }
+        }
+        __syncthreads();
+        // the passes the reference makes (:668-672), replayed on the counts: J passes, then finish (1),
+        // the careful phase (2), or more full passes below D0 (3)
+        int J = 0, mode = 0, S = s_dc[0][0];
+        {
+            int sprev = S, n1 = 0;
+            for (int j = 1;; ++j) {
+                if (j > D0) {
+                    J = D0;
+                    mode = 3;
+                    S = sprev;
+                    break;
+                }
+                n1 += s_dc[1][j - 1];
+                const int Sj = s_dc[0][j] + n1;
+                if (Sj >= N || Sj == sprev) {
+                    J = j;
+                    mode = 1;
+                    S = Sj;
+                    break;
+                }
+                if (Sj + 3 * s_dc[2][j] > N) {
+                    J = j;
+                    mode = 2;
+                    S = Sj;
+                    break;
+                }
+                sprev = Sj;
+            }
+        }
+        uint64_t* cur = lst;
+        uint64_t* nxt = d.lst2;
+        // the list after pass J: depth J (every created node), then depths J-1 .. 0 (single-key nodes)
+        {
+            int v[EP], dk[EP], ik[EP];
+#pragma unroll
+            for (int k = 0; k < EP; ++k) {
+                const int f = t * EP + k;
+                int o = 0, dd = -1, r = 0;
+                for (int e = J; e >= 0; --e) {
+                    const int P = L.n_ini << (2 * e);
+                    if (dd < 0 && f < o + P) {
+                        dd = e;
+                        r = f - o;
+                    }
+                    o += P;
+                }
+                int i = 0, c = 0, pc = 2;
+                if (dd >= 0) {
+                    const int sh = 2 * dd;
+                    const int colp = r >> sh;
+                    const int col = (dd & 1) ? L.n_ini - 1 - colp : colp;
+                    i = (col << sh) | ((r & ((1 << sh) - 1)) ^ (0x33333333 & ((1 << sh) - 1)));
+                    c = ncnt(dd, i);
+                    if (dd) pc = ncnt(dd - 1, i >> 2);
+                }
+                dk[k] = dd;
+                ik[k] = i;
+                v[k] = dd >= 0 && c >= 1 && pc >= 2 && (dd == J || c == 1);
+            }
+            int fl[EP];
+#pragma unroll
+            for (int k = 0; k < EP; ++k) fl[k] = v[k];
+            bscan(v);
+#pragma unroll
+            for (int k = 0; k < EP; ++k)
+                if (fl[k] && v[k] < CAPL) cur[v[k]] = pack((uint32_t)ik[k] << (2 * (D - dk[k])), ncnt(dk[k], ik[k]), dk[k]);
+        }
+        if (S > CAPL) {  // cannot happen (S <= N or <= 4 nIni, both within kp_cap <= CAPL)
+            if (t == 0) atomicOr(overflow, 4);
+            S = CAPL;
+            mode = 1;
+        }
+        int C = s_dc[0][J];
+        __syncthreads();
         mark(2);
-        // the four children's key counts of the node at position e (registers code, count, depth)
-        auto child_counts = [&](uint32_t code, int dp, int e) {
+        // children counts of node p of list l (registers: code, depth)
+        auto child_counts = [&](uint32_t code, int dp, int p) {
             int4 cc;
             if (dp < D0) {
                 const int lo = (int)(code >> bsh), w = 1 << (2 * (D0 - dp - 1));
                 const int c0 = cum(lo), c1 = cum(lo + w), c2 = cum(lo + 2 * w), c3 = cum(lo + 3 * w), c4 = cum(lo + 4 * w);
                 cc = int4{c1 - c0, c2 - c1, c3 - c2, c4 - c3};
             } else {
-                const uint32_t a = d.c4[2 * e], b = d.c4[2 * e + 1];
+                const uint32_t a = d.c4[2 * p], b = d.c4[2 * p + 1];
                 cc = int4{(int)(a & 0xFFFFu), (int)(a >> 16), (int)(b & 0xFFFFu), (int)(b >> 16)};
             }
             return cc;
         };
         auto nonempty = [](const int4& cc) { return (cc.x > 0) + (cc.y > 0) + (cc.z > 0) + (cc.w > 0); };
-        // children counts of the nodes deeper than D0 among the division candidates (cand[k]): one sweep of
-        // every wave over the cached keys
-        auto deep_counts = [&](const bool (&cand)[NP]) {
-            bool any = false;
+        // children counts of the nodes deeper than D0 among the division candidates sel(p): one sweep of every
+        // thread over the cached keys
+        auto deep_counts = [&](auto&& sel) {
+            if (t == 0) s_m[0] = 0;
+            __syncthreads();
 #pragma unroll
-            for (int k = 0; k < NP; ++k) any |= cand[k] && rd(k) >= D0;
-            if (!__ballot(any)) return;
-            int dk[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) dk[k] = cand[k] && rd(k) >= D0;
-            int o[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) o[k] = dk[k];
-            const int nd = chunk_excl_scan(o);
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                if (dk[k]) {
-                    const int e = t * NP + k;
-                    d.dl[o[k]] = e;
-                    d.c4[2 * e] = 0u;
-                    d.c4[2 * e + 1] = 0u;
-                    atomicOr(&d.bins[rc[k] >> bsh], kObDeep);
+            for (int k = 0; k < LP; ++k) {
+                const int p = t * LP + k;
+                if (sel(p) && node_dep(cur, p) >= D0) {
+                    d.dl[atomicAdd(&s_m[0], 1)] = p;
+                    d.c4[2 * p] = 0u;
+                    d.c4[2 * p + 1] = 0u;
+                    atomicOr(&d.bins[node_code(cur, p) >> bsh], kObDeep);
                 }
-            if (t == 0) {
-                s_cmd = 1;
-                s_nd = nd;
             }
-            __syncthreads();  // the other waves start the sweep
-            deep_sweep_l(nd);
-            __syncthreads();  // every wave's counts are in
-            for (int i = t; i < nd; i += 64) atomicAnd(&d.bins[node_code(d.dl[i]) >> bsh], ~kObDeep);
-            wsync();
+            __syncthreads();
+            const int nd = s_m[0];
+            if (nd == 0) return;
+            deep_sort_l(nd, cur);
+            __syncthreads();
+            for_cached(t, NT, std::integral_constant<int, 1>{}, [&](int kk, uint32_t, uint32_t cd) {
+                if (kk >= K || !(d.bins[cd >> bsh] & kObDeep)) return;
+                const int p = deep_find_l(nd, cd, cur);
+                if (p >= 0) {
+                    const int q = (int)((cd >> (2 * (D - node_dep(cur, p) - 1))) & 3u);
+                    atomicAdd(&d.c4[2 * p + (q >> 1)], (q & 1) ? 0x10000u : 1u);
+                }
+            });
+            __syncthreads();
+            for (int i = t; i < nd; i += NT) atomicAnd(&d.bins[node_code(cur, d.dl[i]) >> bsh], ~kObDeep);
+            __syncthreads();
         };
-        int C = 0, phase = 0;
-        bool done = false;
-        for (int iter = 0; !done; ++iter) {
-            if (iter > 4 * CAP + 64) {  // cannot happen (each pass grows the list or finishes); never hang
+        // writes node p's children (counts cc, already known non-empty count) to nxt from position top
+        // downwards: push_front of n1 .. n4 (:620-659, :690-725)
+        auto put_children = [&](uint32_t code, int dp, const int4& cc, int top) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = q == 0 ? cc.x : q == 1 ? cc.y : q == 2 ? cc.z : cc.w;
+                if (n > 0) nxt[top--] = pack(code | ((uint32_t)q << (2 * (D - dp - 1))), n, dp + 1);
+            }
+        };
+        bool ovf = false;
+        for (int iter = 0; mode >= 2; ++iter) {
+            if (iter > 4 * CAPL + 64) {  // cannot happen (each pass grows the list or finishes); never hang
                 if (t == 0) atomicOr(overflow, 2);
                 break;
             }
             mark(8 + 4 * iter);
-            int nck[NP], kep[NP];
-            bool div[NP];
-            int Cn, Kk, nexp = 0;
-            int cbase[NP];
-            if (phase == 0) {
-                // ---------------- full pass (:605-664): divide every node holding more than one key
+            int Sn, Cn;
+            if (mode == 3) {
+                // ---------------- a full pass below D0 (:605-664): divide every node holding > 1 key
+                deep_counts([&](int p) { return p < S && node_cnt(cur, p) > 1; });
+                int cb[LP], kp[LP], ne = 0;
 #pragma unroll
-                for (int k = 0; k < NP; ++k) div[k] = t * NP + k < S && rn(k) > 1;
-                deep_counts(div);
-                int ne = 0;
-#pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    const int4 cc = div[k] ? child_counts(rc[k], rd(k), t * NP + k) : int4{0, 0, 0, 0};
-                    nck[k] = nonempty(cc);
+                for (int k = 0; k < LP; ++k) {
+                    const int p = t * LP + k;
+                    const int n = p < S ? node_cnt(cur, p) : 0;
+                    const int4 cc = n > 1 ? child_counts(node_code(cur, p), node_dep(cur, p), p) : int4{0, 0, 0, 0};
+                    cb[k] = nonempty(cc);
                     ne += (cc.x > 1) + (cc.y > 1) + (cc.z > 1) + (cc.w > 1);
-                    kep[k] = t * NP + k < S && rn(k) == 1;
-                    cbase[k] = nck[k];
+                    kp[k] = n == 1;
                 }
-                Cn = chunk_excl_scan(cbase);
-                Kk = chunk_excl_scan(kep);
-                nexp = wave_total_dpp(ne);
+                int nev[1] = {ne};
+                const int nexp = bscan(nev);
+                Cn = bscan(cb);
+                const int Kk = bscan(kp);
+                Sn = Cn + Kk;
+                if (Sn <= CAPL) {
+#pragma unroll
+                    for (int k = 0; k < LP; ++k) {
+                        const int p = t * LP + k;
+                        const int n = p < S ? node_cnt(cur, p) : 0;
+                        if (n > 1)
+                            put_children(node_code(cur, p), node_dep(cur, p),
+                                         child_counts(node_code(cur, p), node_dep(cur, p), p), Cn - 1 - cb[k]);
+                        else if (n == 1)
+                            nxt[Cn + kp[k]] = cur[p];
+                    }
+                }
+                if (Sn > CAPL) { ovf = true; mode = 0; }
+                else if (Sn >= N || Sn == S) mode = 0;              // :668-671
+                else if (Sn + 3 * nexp > N) mode = 2;               // :672
             } else {
                 // ---------------- careful phase (:675-736): the expandable nodes of the last step (its
-                // children, positions < C) by size descending, equal sizes in creation order descending
-                // (= position ascending); divided until the list reaches N.  Sizes are taken group by group
-                // (wave maximum of the remaining sizes), a group in position order.
-                bool cand[NP];
-                int rem[NP];
-#pragma unroll
-                for (int k = 0; k < NP; ++k) cand[k] = t * NP + k < C && rn(k) > 1;
+                // children, positions < C) by size descending, equal sizes in creation order descending (=
+                // position ascending), divided until the list reaches N
+                auto cand = [&](int p) { return p < C && node_cnt(cur, p) > 1; };
                 deep_counts(cand);
+                // candidates in position order -> (size, position | children << 16) at their compacted index
+                int mi[LP], ncl[LP];
+                int mx = 0;
 #pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    nck[k] = cand[k] ? nonempty(child_counts(rc[k], rd(k), t * NP + k)) : 0;
-                    rem[k] = cand[k] ? rn(k) : 0;
-                    div[k] = false;
-                    cbase[k] = 0;
+                for (int k = 0; k < LP; ++k) {
+                    const int p = t * LP + k;
+                    const bool c = cand(p);
+                    ncl[k] = c ? nonempty(child_counts(node_code(cur, p), node_dep(cur, p), p)) : 0;
+                    mi[k] = c;
+                    if (c) mx = max(mx, node_cnt(cur, p));
                 }
-                int Scur = S, Cacc = 0;
-                for (;;) {
-                    int m = 0;
+                int cf[LP];
 #pragma unroll
-                    for (int k = 0; k < NP; ++k) m = max(m, rem[k]);
-                    const int v = wave_max_dpp(m);
-                    if (v == 0) break;
-                    int x[NP], y[NP];
-                    int gl = 0;
+                for (int k = 0; k < LP; ++k) cf[k] = mi[k];
+                if (t == 0) s_m[1] = 0;
+                const int M = bscan(mi);  // (its barriers order s_m[1]'s reset before the maxima)
+                if (mx) atomicMax(&s_m[1], mx);
+                int* ka = d.sa;  // sizes (ping-pong: ka / kb) and payloads (pa / pb)
+                int* kb = d.sb;
+                int* pa = d.sd;
+                int* pb = d.sp;
 #pragma unroll
-                    for (int k = 0; k < NP; ++k) {
-                        const bool gk = rem[k] == v;
-                        x[k] = gk ? nck[k] : 0;
-                        y[k] = gk ? nck[k] - 1 : 0;
-                        gl += gk;
+                for (int k = 0; k < LP; ++k)
+                    if (cf[k]) {
+                        const int p = t * LP + k;
+                        ka[mi[k]] = node_cnt(cur, p);
+                        pa[mi[k]] = p | (ncl[k] << 16);
                     }
-                    chunk_excl_scan(x);
-                    chunk_excl_scan(y);
-                    int pl = 0, grow = 0, ch = 0;
+                __syncthreads();
+                // stable LSD radix sort by size, descending, 4-bit digits while the largest size has any
+                for (int sh = 0; sh < 32 && (s_m[1] >> sh) != 0; sh += 4) {
+                    int dg[LP], rk[LP];
 #pragma unroll
-                    for (int k = 0; k < NP; ++k)
-                        if (rem[k] == v) {
-                            if (Scur + y[k] < N) {  // the list before it is below N: divided (:729-730)
-                                div[k] = true;
-                                cbase[k] = Cacc + x[k];
-                                ++pl;
-                                grow += nck[k] - 1;
-                                ch += nck[k];
+                    for (int k = 0; k < LP; ++k) {
+                        const int e = t * LP + k;
+                        dg[k] = e < M ? 15 - ((ka[e] >> sh) & 15) : -1;
+                        rk[k] = 0;
+                    }
+                    for (int b = 0; b < 16; ++b) {
+                        int acc = 0;
+                        uint64_t mk[LP];
+#pragma unroll
+                        for (int k = 0; k < LP; ++k) mk[k] = __ballot(dg[k] == b);
+                        int below = 0, tot = 0;
+#pragma unroll
+                        for (int k = 0; k < LP; ++k) {
+                            below += __popcll(mk[k] & lt);
+                            tot += __popcll(mk[k]);
+                        }
+#pragma unroll
+                        for (int k = 0; k < LP; ++k) {
+                            if (dg[k] == b) rk[k] = below + acc;
+                            acc += dg[k] == b;
+                        }
+                        if (lane == 0) s_cw[wv][b] = tot;
+                    }
+                    __syncthreads();
+                    if (t < 64) {  // offset of (wave w, digit b): every smaller digit, then earlier waves
+                        int tot = 0;
+                        if (t < 16)
+                            for (int w = 0; w < NW; ++w) {
+                                s_co[w][t] = tot;
+                                tot += s_cw[w][t];
                             }
-                            rem[k] = 0;
+                        const int base = wave_incl_scan_dpp(tot) - tot;  // digits below t (lanes >= 16: 0)
+                        if (t < 16)
+                            for (int w = 0; w < NW; ++w) s_co[w][t] += base;
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int k = 0; k < LP; ++k)
+                        if (dg[k] >= 0) {
+                            const int e = t * LP + k, o = s_co[wv][dg[k]] + rk[k];
+                            kb[o] = ka[e];
+                            pb[o] = pa[e];
                         }
-                    const int np = wave_total_dpp(pl), ng = wave_total_dpp(gl);
-                    Scur += wave_total_dpp(grow);
-                    Cacc += wave_total_dpp(ch);
-                    if (np < ng || Scur >= N) break;
+                    __syncthreads();
+                    int* tk = ka; ka = kb; kb = tk;
+                    int* tp = pa; pa = pb; pb = tp;
                 }
-                Cn = Cacc;
+                // growth (children - 1) and children in processing order: a candidate is divided iff the list
+                // before it is below N (:729-730); the divided ones are a prefix
+                int gv[LP];
 #pragma unroll
-                for (int k = 0; k < NP; ++k) kep[k] = t * NP + k < S && !div[k];
-                Kk = chunk_excl_scan(kep);
-            }
-            const int Sn = Cn + Kk;
-            if (Sn > CAP) {
-                ovf = true;
-                done = true;
-            } else {
-                // scatter: children in reverse creation order at the front (push_front, :620-659 / :690-725),
-                // the nodes not divided behind them in list order
+                for (int k = 0; k < LP; ++k) {
+                    const int e = t * LP + k;
+                    const int nc = e < M ? pa[e] >> 16 : 0;
+                    gv[k] = e < M ? (nc - 1) | (nc << 16) : 0;
+                }
+                bscan(gv);
+                if (t == 0) s_m[3] = 0;
+                __syncthreads();
 #pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    if (div[k]) {  // the children counts again (LDS reads) rather than 4 NP more registers
-                        int c = cbase[k];
-                        const int dp = rd(k);
-                        const uint32_t code = rc[k];
-                        const int4 cc = child_counts(code, dp, t * NP + k);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int n = q == 0 ? cc.x : q == 1 ? cc.y : q == 2 ? cc.z : cc.w;
-                            if (n > 0) lst[Cn - 1 - c++] = pack(code | ((uint32_t)q << (2 * (D - dp - 1))), n, dp + 1);
-                        }
-                    } else if (t * NP + k < S) {
-                        lst[Cn + kep[k]] = (uint64_t)rc[k] | ((uint64_t)rh[k] << 32);
+                for (int k = 0; k < LP; ++k) {
+                    const int e = t * LP + k;
+                    if (e < M && S + (gv[k] & 0xFFFF) < N) {
+                        atomicMax(&s_m[3], (gv[k] >> 16) + (pa[e] >> 16));  // children up to and including it
+                        d.proc[pa[e] & 0xFFFF] = 1;
                     }
                 }
-                wsync();
-                load_list(Sn);
-                if (phase == 0) {
-                    if (Sn >= N || Sn == S) done = true;              // :668-671
-                    else if (Sn + 3 * nexp > N) phase = 1;            // :672
-                } else if (Sn >= N || Sn == S) {
-                    done = true;                                      // :733-734
+                __syncthreads();
+                Cn = s_m[3];
+                int kp[LP];
+#pragma unroll
+                for (int k = 0; k < LP; ++k) {
+                    const int p = t * LP + k;
+                    kp[k] = p < S && !d.proc[p];
                 }
+                const int Kk = bscan(kp);
+                Sn = Cn + Kk;
+                if (Sn <= CAPL) {
+#pragma unroll
+                    for (int k = 0; k < LP; ++k) {
+                        const int e = t * LP + k;
+                        if (e < M && S + (gv[k] & 0xFFFF) < N) {
+                            const int p = pa[e] & 0xFFFF;
+                            put_children(node_code(cur, p), node_dep(cur, p),
+                                         child_counts(node_code(cur, p), node_dep(cur, p), p), Cn - 1 - (gv[k] >> 16));
+                        }
+                        const int p = t * LP + k;
+                        if (p < S && !d.proc[p]) nxt[Cn + kp[k]] = cur[p];
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < LP; ++k)
+                    if (t * LP + k < S) d.proc[t * LP + k] = 0;
+                if (Sn > CAPL) { ovf = true; mode = 0; }
+                else if (Sn >= N || Sn == S) mode = 0;             // :733-734
+            }
+            __syncthreads();
+            mark(9 + 4 * iter);
+            if (Sn <= CAPL) {
+                uint64_t* tl = cur; cur = nxt; nxt = tl;
                 S = Sn;
                 C = Cn;
             }
         }
-        if (__ballot(ovf) && t == 0) atomicOr(overflow, 4);
+        if (ovf && t == 0) atomicOr(overflow, 4);
         // nodes deeper than D0 of the final list, for the final map
-        int o[NP], dk[NP];
+        if (t == 0) s_m[0] = 0;
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < NP; ++k) o[k] = dk[k] = t * NP + k < S && rd(k) > D0;
-        const int nd = chunk_excl_scan(o);
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            if (dk[k]) d.dl[o[k]] = t * NP + k;
+        for (int k = 0; k < LP; ++k) {
+            const int p = t * LP + k;
+            if (p < S && node_dep(cur, p) > D0) d.dl[atomicAdd(&s_m[0], 1)] = p;
+        }
+        __syncthreads();
         if (t == 0) {
             s_S = S;
-            s_cur = 0;
-            s_cmd = 0;
+            s_cur = cur == lst ? 0 : 1;
+            s_nd = s_m[0];
         }
-        __syncthreads();  // the other waves leave their command loop
-        if (t == 0) s_nd = nd;
+    } else if (t >= 64) {
+        for (;;) {
+            __syncthreads();  // a command (deep_counts) or the end of the passes
+            const int cmd = s_cmd;
+            if (cmd == 0) break;
+            deep_sweep(s_nd, cmd >> 1);
+            __syncthreads();  // sweep complete
+        }
     } else {
         wave_scan_lds((int*)d.bins, B);
         if (t == 0) d.bins[B] = (uint32_t)K;
@@ -2498,8 +2680,9 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     const int S = s_S, nd = s_nd;
     const uint32_t* code = s_cur ? d.code1 : d.code0;
     const uint8_t* dep = s_cur ? d.dep1 : d.dep0;
-    auto fcode = [&](int p) { return REG ? node_code(p) : code[p]; };
-    auto fdep = [&](int p) { return REG ? node_dep(p) : (int)dep[p]; };
+    const uint64_t* flst = s_cur ? d.lst2 : lst;
+    auto fcode = [&](int p) { return FLAT ? node_code(flst, p) : code[p]; };
+    auto fdep = [&](int p) { return FLAT ? node_dep(flst, p) : (int)dep[p]; };
     uint32_t* best = (uint32_t*)d.sa;
     // a node of depth <= D0 covers whole bins: its best key is the maximum of their maxima
     for (int p = t; p < S; p += NT) {
@@ -2519,12 +2702,12 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         __syncthreads();
     }
     if (nd > 0) {
-        if constexpr (REG) deep_sort_l(nd);
+        if constexpr (FLAT) deep_sort_l(nd, flst);
         else deep_sort(nd, code);
         __syncthreads();
         for_cached(t, NT, std::integral_constant<int, 2>{}, [&](int kk, uint32_t v, uint32_t cd) {
             if (kk >= K || d.bins[cd >> bsh] != kObDeep) return;
-            const int q = REG ? deep_find_l(nd, cd) : deep_find(nd, code, dep, cd);
+            const int q = FLAT ? deep_find_l(nd, cd, flst) : deep_find(nd, code, dep, cd);
             if (q >= 0) atomicMax(&best[q], (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)kk));
         });
     }
@@ -2661,6 +2844,9 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <int NT>
+__device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, int* cnt, int* tmp);
+
 // tab: [0, 192) horizontal items (src dword | hbuf uint4 index << 16, ~0 = none), then 256 centroid slots
 // as uint4 (u byte weights, v byte weights, src dword, 0) — built by the host
 // (orbfe_host.hip: orb_tables).
@@ -2669,16 +2855,24 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                                                     const uint8_t* __restrict__ ws, const uint32_t* __restrict__ lvl_kp,
                                                     const int* __restrict__ lvl_count, orbfe_keypoint* __restrict__ out_kp,
                                                     uint8_t* __restrict__ out_desc, int* __restrict__ out_count,
-                                                    const uint32_t* __restrict__ tab) {
+                                                    const uint32_t* __restrict__ tab, int gx, StereoArgs sa, int n_bucket) {
     __shared__ float4 s_pat[256];
     __shared__ uint2 s_cw[64 * kOrbCSlots];                // centroid slot: signed byte weights (u, v)
     __shared__ uint32_t s_src[WAVES][kSrcRows * kSrcDw];  // staged unblurred window
     __shared__ uint32_t s_h[WAVES][kHPairs * kHDw];       // horizontal taps, row-pair interleaved u16
-    const int nb = gridDim.x * gridDim.y, hw = blockIdx.y * gridDim.x + blockIdx.x;
+    // the first n_bucket workgroups build the stereo row buckets of pairs 0 .. n_bucket - 1 (they need the
+    // octree's level keypoints only, stereo_bucket_pair): dispatched first, they run under the descriptor
+    // workgroups instead of as a launch of their own after them (the host fuses only when H + 1 counters fit
+    // s_h and the block is 256 threads)
+    if ((int)blockIdx.x < n_bucket) {
+        if constexpr (WAVES == 4) stereo_bucket_pair<256>(g, sa, blockIdx.x, (int*)&s_h[0][0], (int*)&s_src[0][0]);
+        return;
+    }
+    const int nb = (int)gridDim.x - n_bucket, hw = (int)blockIdx.x - n_bucket;  // 1-D grid: n_bucket + gx images
     const int per = nb >> 3;
     const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;  // XCD-aware: runs of waves per L2
-    const int img = __builtin_amdgcn_readfirstlane(lb / (int)gridDim.x);
-    const int blk = __builtin_amdgcn_readfirstlane(lb - img * (int)gridDim.x);
+    const int img = __builtin_amdgcn_readfirstlane(lb / gx);
+    const int blk = __builtin_amdgcn_readfirstlane(lb - img * gx);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wv = __builtin_amdgcn_readfirstlane(blk * WAVES + wid);
     // the lane's centroid slots: window dword (two 16-bit halves per register), the same for
@@ -3073,47 +3267,81 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // [floor(y - 2s), ceil(y + 2s)] (double arithmetic, s = scale of its octave).  One workgroup per pair:
 // LDS histogram -> block scan -> fill.  The order inside a bucket is irrelevant: k_stereo reduces
 // (distance, iR) lexicographically, which is the reference's first minimum in ascending iR.
-// Also writes the compact (x, octave) record of every right keypoint.  NT = 1 024 threads for small batches:
-// the kernel is one latency chain per pair (load, count, scan, fill), and a frame's one pair waits on it
-// whole; 256 for large ones, whose many workgroups share the CUs with the other streams' stages.
+// Also writes the compact (x, octave) record of every right keypoint.  The right keypoints are read from the
+// octree's level keypoints (lvl_kp, lvl_count: x | y << 12 | score << 24 in level pixels), with the
+// coordinates k_orb will write (ORBextractor.cpp:1094-1100: x = f32(level x) * scale[l] for l > 0) and the
+// index iR = the level-major position — so the buckets need the octree only, and the frame and batch paths
+// build them inside k_orb's launch (extra workgroups, stereo_bucket_pair) instead of after it.
+// cnt: H + 1 ints of LDS, tmp: 257 + 2 kMaxLevels + 1 ints.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_stereo_bucket(Geo g, StereoArgs A) {
-    constexpr int kBkThreads = NT;
-    extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
-    __shared__ int scan_tmp[257];
-    const int pr = blockIdx.x, t = threadIdx.x;
-    const int H = g.H, nR = A.countR[pr * A.cnt_stride];
-    const orbfe_keypoint* KR = A.kpsR + pr * A.kp_stride;
+__device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, int* cnt, int* tmp) {
+    const int t = threadIdx.x;
+    const int H = g.H;
+    const uint32_t* lk = A.lkpR + pr * A.lkp_stride;
+    const int* lc = A.lcntR + pr * A.lcnt_stride;
     int* off = A.bucket_off + (int64_t)pr * (H + 1);
     uint16_t* idx = A.bucket_idx + (int64_t)pr * A.bucket_cap;
     float2* rinfo = A.rinfo + pr * A.out_stride;
-    // per-octave scales in LDS: a lane-indexed read of the kernel argument would be a vector memory load
-    __shared__ float s_scale[kMaxLevels];
+    int* scan_tmp = tmp;
+    float* s_scale = (float*)(tmp + 257);     // per-octave scales (a lane-indexed kernel-argument read would be
+    int* s_pre = tmp + 257 + kMaxLevels;     // a vector memory load); first right keypoint of every level
     if (t < kMaxLevels) s_scale[t] = g.scale[t];
-    for (int i = t; i <= H; i += kBkThreads) cnt[i] = 0;
+    if (t == 0) {
+        int p0 = 0;
+        for (int l = 0; l < kMaxLevels; ++l) {
+            s_pre[l] = p0;
+            p0 += l < g.nlevels ? lc[l] : 0;
+        }
+        s_pre[kMaxLevels] = p0;
+    }
+    for (int i = t; i <= H; i += NT) cnt[i] = 0;
     __syncthreads();
-    for (int i = t; i < nR; i += kBkThreads) {
-        const orbfe_keypoint kr = KR[i];
-        rinfo[i] = make_float2(kr.x, __int_as_float(kr.octave));
-        const double r = 2.0 * (double)s_scale[kr.octave];
-        const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
-        for (int y = lo; y <= hi; ++y) atomicAdd(&cnt[y], 1);
+    const int nR = s_pre[kMaxLevels];
+    // right keypoint i: its octave, y (as k_orb computes it) and x
+    auto right_kp = [&](int i, int& l, float& x, float& y) {
+        l = 0;
+#pragma unroll
+        for (int j = 1; j < kMaxLevels; ++j) l += j < g.nlevels && s_pre[j] <= i;
+        const uint32_t key = lk[g.lv[l].kp_off + (i - s_pre[l])];
+        const float xl = (float)(int)(key & 0xFFFu), yl = (float)(int)((key >> 12) & 0xFFFu);
+        x = l ? __fmul_rn(xl, s_scale[l]) : xl;
+        y = l ? __fmul_rn(yl, s_scale[l]) : yl;
+    };
+    for (int i = t; i < nR; i += NT) {
+        int l;
+        float x, y;
+        right_kp(i, l, x, y);
+        rinfo[i] = make_float2(x, __int_as_float(l));
+        const double r = 2.0 * (double)s_scale[l];
+        const int lo = max((int)floor((double)y - r), 0), hi = min((int)ceil((double)y + r), H - 1);
+        for (int yy = lo; yy <= hi; ++yy) atomicAdd(&cnt[yy], 1);
     }
     __syncthreads();
     const int total = block_excl_scan(cnt, H, scan_tmp);
     if (t == 0) cnt[H] = total;
     __syncthreads();
-    for (int i = t; i <= H; i += kBkThreads) off[i] = cnt[i];
+    for (int i = t; i <= H; i += NT) off[i] = cnt[i];
     __syncthreads();
-    for (int i = t; i < nR; i += kBkThreads) {
-        const orbfe_keypoint kr = KR[i];
-        const double r = 2.0 * (double)s_scale[kr.octave];
-        const int lo = max((int)floor((double)kr.y - r), 0), hi = min((int)ceil((double)kr.y + r), H - 1);
-        for (int y = lo; y <= hi; ++y) {
-            const int pos = atomicAdd(&cnt[y], 1);
+    for (int i = t; i < nR; i += NT) {
+        int l;
+        float x, y;
+        right_kp(i, l, x, y);
+        const double r = 2.0 * (double)s_scale[l];
+        const int lo = max((int)floor((double)y - r), 0), hi = min((int)ceil((double)y + r), H - 1);
+        for (int yy = lo; yy <= hi; ++yy) {
+            const int pos = atomicAdd(&cnt[yy], 1);
             if (pos < A.bucket_cap) idx[pos] = (uint16_t)i;
         }
     }
+}
+
+// The buckets as a kernel of their own (the separate extract / stereo calls, orbfe_stereo_match).  NT = 1 024
+// threads for small batches: one latency chain per pair (load, count, scan, fill); 256 for large ones.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_stereo_bucket(Geo g, StereoArgs A) {
+    extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
+    __shared__ int tmp[257 + 2 * kMaxLevels + 1];
+    stereo_bucket_pair<NT>(g, A, blockIdx.x, cnt, tmp);
 }
 
 // Four left keypoints per wavefront, 16 lanes each (Frame.py:186-278); row q = lane >> 4 of the wave.
@@ -3661,11 +3889,16 @@ static int orb_waves(const Geo& g, int kpw) {
 template <int NW, int KPW>
 static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                           const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
-                          const uint32_t* tab, hipStream_t s) {
+                          const uint32_t* tab, hipStream_t s, const StereoArgs* bucket, int n_bucket) {
     const int waves = orb_waves(g, KPW);  // most waves an image can need: KPW keypoints per wave, per level
-    hipLaunchKernelGGL((k_orb<NW, KPW>), dim3((waves + NW - 1) / NW, n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws,
-                       lvl_kp, lvl_count, out_kp, out_desc, out_count, tab);
+    const int gx = (waves + NW - 1) / NW;
+    const int nbk = bucket && NW == 4 ? n_bucket : 0;
+    hipLaunchKernelGGL((k_orb<NW, KPW>), dim3(nbk + gx * n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws, lvl_kp,
+                       lvl_count, out_kp, out_desc, out_count, tab, gx, bucket ? *bucket : StereoArgs{}, nbk);
 }
+
+// k_orb can carry the stereo buckets when the (H + 1) counters fit its s_h buffer (256-thread workgroups)
+bool orb_fuses_bucket(const Geo& g) { return g.H + 1 <= 4 * kHPairs * kHDw; }
 
 // keypoints per wave for a batch: 8 (4 waves per workgroup: 953 -> 914 us per 256 pairs against 4, same-box
 // A/B, round 1) while the batch gives >= 16 waves per CU that way, else 4, else 2 (a frame pair: 508 waves of
@@ -3681,27 +3914,33 @@ int orb_kpw(const Geo& g, int n_images, int variant) {
 
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
                       const int* lvl_count, orbfe_keypoint* out_kp, uint8_t* out_desc, int* out_count, int n_images,
-                      const uint32_t* tab, hipStream_t s, int variant) {
+                      const uint32_t* tab, hipStream_t s, int variant, const StereoArgs* bucket, int n_bucket) {
+    if (bucket && !orb_fuses_bucket(g)) return hipErrorInvalidValue;
 #ifdef ORBFE_DEV_VARIANTS
     if (variant == 8) {
-        launch_orb_nw<8, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        launch_orb_nw<8, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s, nullptr, 0);
         return hipGetLastError();
     }
     if (variant == 10) {
-        launch_orb_nw<4, 16>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        launch_orb_nw<4, 16>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s, bucket,
+                             n_bucket);
         return hipGetLastError();
     }
 #endif
     switch (orb_kpw(g, n_images, variant)) {
-        case 2: launch_orb_nw<4, 2>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s); break;
-        case 4: launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s); break;
-        default: launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s);
+        case 2: launch_orb_nw<4, 2>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s,
+                                    bucket, n_bucket); break;
+        case 4: launch_orb_nw<4, 4>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s,
+                                    bucket, n_bucket); break;
+        default: launch_orb_nw<4, 8>(g, in, in_pitch, ws, lvl_kp, lvl_count, out_kp, out_desc, out_count, n_images, tab, s,
+                                     bucket, n_bucket);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s) {
-    if (2 * n_pairs < kSmallBatchImages)
+hipError_t launch_stereo(const Geo& g, const StereoArgs& a, int n_pairs, hipStream_t s, bool buckets_built) {
+    if (buckets_built) {
+    } else if (2 * n_pairs < kSmallBatchImages)
         hipLaunchKernelGGL(k_stereo_bucket<1024>, dim3(n_pairs), dim3(1024), (size_t)4 * (g.H + 1), s, g, a);
     else
         hipLaunchKernelGGL(k_stereo_bucket<256>, dim3(n_pairs), dim3(256), (size_t)4 * (g.H + 1), s, g, a);

@@ -36,7 +36,11 @@ def main():
     m = buf.reshape(2 * a.pairs, 8, 64).astype(np.float64) / 100.0  # us
     t0 = m[:, :, 0:1]
     for l in range(8):
-        ids = [i for i in range(64) if (m[:, l, i] > 0).all()]
+        raw = {i: float(np.median(buf.reshape(2 * a.pairs, 8, 64)[:, l, i])) for i in range(40, 50)
+               if (buf.reshape(2 * a.pairs, 8, 64)[:, l, i] > 0).any() and (buf.reshape(2 * a.pairs, 8, 64)[:, l, i] < 10000).all()}
+        if raw:
+            print(f"level {l} counters: " + " ".join(f"{i}:{v:.0f}" for i, v in raw.items()))
+        ids = [i for i in range(64) if (m[:, l, i] > 0).all() and not (40 <= i < 50 and i in raw)]
         rel = {i: float(np.median(m[:, l, i] - m[:, l, 0])) for i in ids}
         print(f"level {l}: " + " ".join(f"{i}:{v:.1f}" for i, v in rel.items()))
     tot = m[:, :, 63] - m[:, :, 0]
