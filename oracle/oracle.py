@@ -98,6 +98,9 @@ class OracleExtractor:
         n = C.c_int32()
         rc = lib().oracle_extract(C.byref(self.p), _ptr(image), w, h, w, _ptr(kps), _ptr(desc), cap, C.byref(n),
                                   _ptr(pyr))
+        if rc == -1 and w and h:
+            raise ValueError("the reference's DistributeOctTree refuses this geometry (vpIniNodes.resize of a negative "
+                             "nIni, ORBextractor.cpp:543-550: std::length_error)")
         if rc != 0:
             raise RuntimeError(f"oracle_extract failed: {rc}")
         self._pyr = []

@@ -176,9 +176,36 @@ struct Image {
     const uint8_t* row(int y) const { return px.data() + (size_t)y * w; }
 };
 
+// ---------------------------------------------------------------- cv::resize INTER_AREA fast path, 8U
+// cv::resize switches INTER_LINEAR with an exact 2x step (|scale - 2| < DBL_EPSILON both ways) to INTER_AREA,
+// whose fast path (resizeAreaFast_Invoker + ResizeAreaFastVec_SIMD_8u, OpenCV 4.x imgproc/resize.cpp) averages
+// every 2 x 2 block: the vector loop (u16 lanes = simd / 2 per step, while dx <= w - lanes) stores
+// v_rshr_pack_store<2>, i.e. (a + b + c + d + 2) >> 2; the scalar tail saturate_cast<uchar>(sum * 0.25f), i.e.
+// sum / 4 rounded half to even.  Parity unpinned (OpenCV is absent), like the linear path.
+void resize_area2(const uint8_t* src, int sw, int sstride, uint8_t* dst, int dw, int dh, int simd) {
+    (void)sw;
+    const int lanes = simd / 2;
+    const int xv = lanes > 0 ? dw / lanes * lanes : 0;
+    for (int dy = 0; dy < dh; ++dy) {
+        const uint8_t* S0 = src + (size_t)(2 * dy) * sstride;
+        const uint8_t* S1 = S0 + sstride;
+        for (int dx = 0; dx < dw; ++dx) {
+            const int sum = S0[2 * dx] + S0[2 * dx + 1] + S1[2 * dx] + S1[2 * dx + 1];
+            dst[(size_t)dy * dw + dx] = dx < xv ? (uint8_t)((sum + 2) >> 2) : sat_u8(round_even_f((float)sum * 0.25f));
+        }
+    }
+}
+
 // ---------------------------------------------------------------- cv::resize INTER_LINEAR, 8U
 void resize_linear(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh, int simd) {
     const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    {
+        const int isx = (int)std::lrint(scale_x), isy = (int)std::lrint(scale_y);
+        if (std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON && isx == 2 && isy == 2) {
+            resize_area2(src, sw, sstride, dst, dw, dh, simd);
+            return;
+        }
+    }
     std::vector<int> xofs(dw);
     std::vector<short> ax(2 * dw);
     int xmax = dw;
@@ -674,9 +701,28 @@ int oracle_octree(const int32_t* xyr, int32_t n, int32_t minX, int32_t maxX, int
     return (int)sel.size();
 }
 
+// The reference runs DistributeOctTree on every level, with or without cells: nIni = round((float)(maxX -
+// minX) / (maxY - minY)) sizes vpIniNodes.resize(nIni) (ORBextractor.cpp:543-550), which throws
+// std::length_error when nIni < 0 (a level lower than 32 px but wider) and is undefined when maxY == minY; a
+// level with cells and nIni == 0 indexes vpIniNodes out of range (:557).  Such geometries are refused.
+bool reference_geometry_ok(const Config& C, int W, int H) {
+    for (int l = 0; l < C.nlevels; ++l) {
+        const int w = round_even_f((float)W * C.isf[l]), h = round_even_f((float)H * C.isf[l]);
+        if (w < 1 || h < 1) return false;  // cv::resize of an empty size asserts
+        const int sx = (w - kEdge + 3) - (kEdge - 3), sy = (h - kEdge + 3) - (kEdge - 3);
+        if (sy == 0) return false;
+        const float q = std::round((float)sx / (float)sy);
+        if (!std::isfinite(q) || q < 0.f) return false;
+        const int nCols = (int)((float)sx / 30.f), nRows = (int)((float)sy / 30.f);
+        if (nCols > 0 && nRows > 0 && (int)q == 0) return false;
+    }
+    return true;
+}
+
 int oracle_octree_ties(const orbfe_params* p, const uint8_t* img, int32_t w, int32_t h, int32_t stride, int32_t* ties) {
     Config C;
     if (!make_config(p, C) || !ties) return ORBFE_EINVAL;
+    if (w > 0 && h > 0 && !reference_geometry_ok(C, w, h)) return ORBFE_EINVAL;
     for (int l = 0; l < 5 * C.nlevels; ++l) ties[l] = 0;
     if (w <= 0 || h <= 0) return ORBFE_OK;
     std::vector<Image> pyr;
@@ -702,6 +748,7 @@ int oracle_extract(const orbfe_params* p, const uint8_t* img, int32_t w, int32_t
     if (!make_config(p, C) || !n_out) return ORBFE_EINVAL;
     *n_out = 0;
     if (w <= 0 || h <= 0) return ORBFE_OK;  // _image.empty() -> return (:1045-1046)
+    if (!reference_geometry_ok(C, w, h)) return ORBFE_EINVAL;
     std::vector<Image>& pyr = g_lastPyr;
     build_pyramid(C, img, w, h, stride, pyr);
     if (pyr_out) {

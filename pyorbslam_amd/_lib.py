@@ -162,9 +162,17 @@ def pyhost():
     return _pyhost
 
 
+class OrbfeGeometryError(OrbfeError, ValueError):
+    """A level geometry the reference's DistributeOctTree cannot take (vpIniNodes.resize of a negative nIni,
+    ORBextractor.cpp:543-550): the reference throws std::length_error, which pybind11 raises as ValueError."""
+
+
 def check(fn: str, rc: int) -> None:
     if rc != ORBFE_OK:
-        raise OrbfeError(fn, rc, lib().orbfe_last_error().decode(errors="replace"))
+        msg = lib().orbfe_last_error().decode(errors="replace")
+        if rc == -1 and "DistributeOctTree" in msg:  # EINVAL
+            raise OrbfeGeometryError(fn, rc, msg)
+        raise OrbfeError(fn, rc, msg)
 
 
 def call(name: str, *args) -> None:

@@ -40,6 +40,8 @@ struct LevelGeo {
     int xtab_off, ytab_off;
     int xmax;            // first column whose sx+1 >= src width
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
+    int area;            // 1: an exact 2x step, cv::resize's INTER_AREA fast path (resizeAreaFast_): the tables
+                         // hold the 2x2 average (weights 1024), xvec its vector span, the tail rounds half to even
     // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;
     // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
     int rs_ngrp, rs_nsrc, rs_sp;

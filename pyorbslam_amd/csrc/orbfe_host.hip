@@ -221,11 +221,25 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
     const double scale_x = 1. / inv_x, scale_y = 1. / inv_y;
     const int isx = (int)std::lrint(scale_x), isy = (int)std::lrint(scale_y);
     const bool area_fast = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON;
-    if (area_fast && isx == 2 && isy == 2)
-        throw Error(ORBFE_EINVAL, "scale factor 2 selects cv::resize's INTER_AREA path, which is not implemented");
     while (xt.size() % 4) xt.push_back(ResizeX{0, 0, 0});  // k_resize reads 4 entries as 2 x 16 bytes
     Lg.xtab_off = (int)xt.size();
     Lg.ytab_off = (int)yt.size();
+    Lg.area = 0;
+    if (area_fast && isx == 2 && isy == 2) {
+        // cv::resize turns INTER_LINEAR with an exact 2x step into INTER_AREA, whose fast path
+        // (resizeAreaFast_, ResizeAreaFastVec_SIMD_8u) averages 2 x 2 blocks: (a + b + c + d + 2) >> 2 over the
+        // vector span (v_rshr_pack_store<2>, u16 lanes = simd / 2 per step), saturate_cast<uchar>(sum * 0.25f)
+        // after it.  As linear tables: sx = 2 dx, sy = 2 dy, 2 dy + 1, all weights 1024 — the kernels' vector
+        // formula (mulhi(H >> 4, b) ...) then is exactly the rounding shift, and resize_tail the half-even tail.
+        Lg.area = 1;
+        for (int dx = 0; dx < dw; ++dx) xt.push_back(ResizeX{2 * dx, 1024, 1024});
+        Lg.xmax = dw;
+        for (int k = 0; k < 4; ++k) xt.push_back(ResizeX{sw - 1, 2048, 0});  // over-read guard, as below
+        const int lanes = simd / 2;
+        Lg.xvec = lanes > 0 ? dw / lanes * lanes : 0;
+        for (int dy = 0; dy < dh; ++dy) yt.push_back(ResizeY{2 * dy, 2 * dy + 1, 1024, 1024});
+        return;
+    }
     int xmax = dw;
     for (int dx = 0; dx < dw; ++dx) {
         float fx = (float)((dx + 0.5) * scale_x - 0.5);
@@ -391,8 +405,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         // gather records (k_detect, k_octree_bins, k_pack_compact)
         if (Lg.w < 1 || Lg.h < 1 || Lg.w > kMaxLevelSide || Lg.h > kMaxLevelSide)
             throw Error(ORBFE_EINVAL, "level size out of range (1..4095 px per side)");
-        if (Lg.w <= kEdge || Lg.h <= kEdge)
-            throw Error(ORBFE_EINVAL, "image too small: a pyramid level is not wider than the 19 px reflect border");
+        // levels of 19 px or less are padded by an iterated reflection (k_shear); they have no FAST cells
         Lg.pitch = (Lg.w + 15) & ~15;
         if (l > 0) {
             Lg.ws_off = ws;
@@ -458,6 +471,19 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         // DistributeOctTree initial columns (:543-545)
         Lg.n_ini = 0;
         Lg.hx = 1.f;
+        {
+            // the reference runs DistributeOctTree on every level, cells or not: nIni = round((float)spanX /
+            // spanY) sizes vpIniNodes.resize(nIni) (:543-550), which throws std::length_error for nIni < 0 (a
+            // level lower than 32 px but wider, e.g. 1241x376 at scaleFactor 2 from its 5th level on) and is
+            // undefined for spanY == 0 (float division by zero): such geometries are refused like the
+            // reference refuses them.  Smaller levels pass (e.g. square ones: nIni = 1).
+            const float q = Lg.span_y != 0 ? std::round((float)Lg.span_x / (float)Lg.span_y) : NAN;
+            if (!std::isfinite(q) || q < 0.f)
+                throw Error(ORBFE_EINVAL, "level " + std::to_string(l) + " (" + std::to_string(Lg.w) + "x" +
+                                              std::to_string(Lg.h) + "): the reference's DistributeOctTree fails "
+                                              "(vpIniNodes.resize(nIni) with nIni = round(spanX / spanY) negative or "
+                                              "undefined, ORBextractor.cpp:543-550)");
+        }
         if (Lg.ncell > 0) {
             if (Lg.span_y <= 0 || Lg.span_x <= 0) throw Error(ORBFE_EINVAL, "degenerate level");
             Lg.n_ini = (int)std::round((float)Lg.span_x / Lg.span_y);

@@ -88,6 +88,24 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p >= n ? 2 * n - 2 - p : p;
 }
 
+// cv::borderInterpolate(BORDER_REFLECT_101) for any overshoot: the reflection iterates (period 2 n - 2), a
+// 1-pixel side maps everything to 0 — the 19-pixel padding of levels up to 19 px (copyMakeBorder,
+// ORBextractor.cpp:1122-1128)
+__device__ __forceinline__ int reflect101_iter(int p, int n) {
+    if (n == 1) return 0;
+    const int per = 2 * n - 2;
+    p = (p < 0 ? -p : p) % per;
+    return p >= n ? per - p : p;
+}
+
+// the scalar tail of the vertical pass: FixedPtCast<int, uchar, 22> (round half up) of INTER_LINEAR, or for
+// the INTER_AREA fast path saturate_cast<uchar>(sum * 0.25f), i.e. sum / 4 rounded half to even (t = sum << 20)
+__device__ __forceinline__ uint32_t resize_tail(uint32_t t, int area) {
+    if (!area) return (t + (1u << 21)) >> 22;
+    const uint32_t q = t >> 22, r = t & 0x3FFFFFu;
+    return q + (r > 0x200000u || (r == 0x200000u && (q & 1u)));
+}
+
 __device__ __forceinline__ const uint8_t* level_ptr(const Geo& g, int l, const uint8_t* in, int64_t in_pitch,
                                                     const uint8_t* ws, int img, int* stride) {
     if (l == 0) {
@@ -295,7 +313,7 @@ __global__ __launch_bounds__(256) void k_resize(Geo g, int l, const uint8_t* __r
         if (dx + 3 >= L.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+                if (dx + k >= L.xvec) v[k] = resize_tail(h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12), L.area);
         }
         // pixels past L.w land in the row's pitch padding
         *(uint32_t*)(dst + rr * L.pitch + dx) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
@@ -436,7 +454,7 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             if (tail) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (dx + k >= L.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+                    if (dx + k >= L.xvec) v[k] = resize_tail(h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12), L.area);
             }
             // pixels past L.w land in the row's pitch padding
             __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
@@ -567,7 +585,7 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
                 if (dx + 3 >= Lv.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if (dx + k >= Lv.xvec) v[k] = (h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12) + (1u << 21)) >> 22;
+                        if (dx + k >= Lv.xvec) v[k] = resize_tail(h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12), Lv.area);
                 }
                 const uint32_t px = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
                 *(lds_w32*)(uintptr_t)(dst_base + (uint32_t)((r - c0) * pitch + dx)) = px;
@@ -3253,7 +3271,7 @@ __global__ __launch_bounds__(256) void k_shear(Geo g, const uint8_t* __restrict_
     for (int b = 0; b < 4 && i + b < n; ++b) {
         const int64_t f = (int64_t)kEdge * pw + kEdge + i + b;
         const int pr = (int)(f / pw), pc = (int)(f - (int64_t)pr * pw);
-        const uint8_t px = lvl[(int64_t)reflect101(pr - kEdge, L.h) * stride + reflect101(pc - kEdge, L.w)];
+        const uint8_t px = lvl[(int64_t)reflect101_iter(pr - kEdge, L.h) * stride + reflect101_iter(pc - kEdge, L.w)];
         v |= (uint32_t)px << (8 * b);
         if (i + 4 > n) o[b] = px;  // the level's last bytes (its region is padded to 4 bytes)
     }

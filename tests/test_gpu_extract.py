@@ -164,6 +164,11 @@ CONFIGS = [
     ((376, 1241), dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=9, minThFAST=9)),
     ((720, 1280), dict(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
     ((1080, 1920), dict(nfeatures=4000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7)),
+    # exact 2x steps (cv::resize's INTER_AREA fast path: 620x188 -> 310x94 -> 155x47; the
+    # first step, 1241 -> 620, is linear), and levels of 19 px or less (iterated reflect-101 padding)
+    ((376, 1241), dict(nfeatures=2000, scaleFactor=2.0, nlevels=4, iniThFAST=20, minThFAST=7)),
+    ((400, 400), dict(nfeatures=1000, scaleFactor=2.0, nlevels=6, iniThFAST=20, minThFAST=7)),
+    ((128, 128), dict(nfeatures=300, scaleFactor=1.2, nlevels=12, iniThFAST=20, minThFAST=7)),
 ]
 
 
@@ -193,3 +198,31 @@ def test_strided_view_input_follows_the_reference_caster():
     assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
     shown, _ = O.OracleExtractor(**KITTI).extract(np.ascontiguousarray(v))
     assert shown.tobytes() != kps.tobytes()
+
+
+@pytest.mark.parametrize("ci", [len(CONFIGS) - 2, len(CONFIGS) - 1])
+def test_tiny_levels_sheared_pyramid(ci):
+    """Levels of 19 px or less: GetImagePyramid's sheared views read the 19-px padding, which reflects more than
+    once (copyMakeBorder REFLECT_101, ORBextractor.cpp:1122-1128) — against the oracle's view of each level."""
+    (h, w), params = CONFIGS[ci]
+    img = synth.make_pair(300 + ci, w, h)[0]
+    ex = ORBextractor(**params)
+    ex.extract(img)
+    oe = O.OracleExtractor(**params)
+    oe.extract(img)
+    got, want = ex.GetImagePyramid(), oe.sheared_pyramid()
+    assert len(got) == len(want) and min(p.shape[0] for p in want) <= 19
+    for l, (a, b) in enumerate(zip(got, want)):
+        assert a.shape == b.shape and np.array_equal(a, b), f"level {l}"
+
+
+def test_reference_refused_geometries_gpu():
+    """A level lower than 32 px but wider makes the reference's DistributeOctTree throw (vpIniNodes.resize of a
+    negative nIni, ORBextractor.cpp:543-550; pybind11 raises std::length_error as ValueError): the drop-in
+    raises ValueError for the same geometries, the oracle too."""
+    for (h, w), prm in (((96, 160), dict(nlevels=12)), ((376, 1241), dict(scaleFactor=2.0, nlevels=8))):
+        img = synth.make_pair(5, w, h)[0]
+        with pytest.raises(ValueError):
+            ORBextractor(**prm).extract(img)
+        with pytest.raises(ValueError):
+            O.OracleExtractor(**prm).extract(img)

@@ -267,7 +267,11 @@ def test_graph_stereo_against_restatement_after_replays():
 
 @pytest.mark.parametrize("shape,params", [((376, 1241), KITTI), ((480, 752), EUROC), ((333, 641), KITTI),
                                           ((157, 211), dict(KITTI, nfeatures=500)), ((400, 2560), KITTI),
-                                          ((376, 1241), dict(KITTI, scaleFactor=1.1, nlevels=12))])
+                                          ((376, 1241), dict(KITTI, scaleFactor=1.1, nlevels=12)),
+                                          # exact 2x steps (INTER_AREA fast path) and levels down to 6 / 17 px
+                                          ((376, 1241), dict(KITTI, scaleFactor=2.0, nlevels=4)),
+                                          ((400, 400), dict(KITTI, nfeatures=1000, scaleFactor=2.0, nlevels=7)),
+                                          ((128, 128), dict(KITTI, nfeatures=300, nlevels=12))])
 def test_resize_cascade_equals_per_level_launches(shape, params):
     """k_resize_cascade (the one-launch pyramid of small batches, strips with halo rows) against the
     per-level k_resize_rows launches and the oracle, at several strip counts (orbfe_microbench stage 0:

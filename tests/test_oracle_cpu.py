@@ -379,3 +379,48 @@ def test_octree_tie_report(kitti_png):
         if ties[l, 1] == 0:
             assert a == b, f"level {l}: no tie run reported, yet the keypoint order differs"
     assert sum(set_differs) > len(set_differs) // 2, set_differs
+
+
+def _area2_py(src, simd):
+    """cv::resize's INTER_AREA fast path for an exact 2x step, from its definition (OpenCV 4.x resize.cpp:
+    resizeAreaFast_Invoker + ResizeAreaFastVec_SIMD_8u): (sum + 2) >> 2 over the vector span, sum * 0.25f rounded
+    half to even after it."""
+    h, w = src.shape[0] // 2, src.shape[1] // 2
+    s = src.astype(np.int32)
+    tot = s[0::2, 0::2][:h, :w] + s[0::2, 1::2][:h, :w] + s[1::2, 0::2][:h, :w] + s[1::2, 1::2][:h, :w]
+    lanes = simd // 2
+    xv = w // lanes * lanes if lanes else 0
+    out = np.rint(tot.astype(np.float32) * np.float32(0.25)).astype(np.int32)  # np.rint: half to even
+    out[:, :xv] = (tot[:, :xv] + 2) >> 2
+    return out.astype(np.uint8)
+
+
+@pytest.mark.parametrize("simd", [0, 16, 32])
+def test_resize_area_fast_path(simd):
+    """an exact 2x step takes OpenCV's INTER_AREA fast path; the two roundings differ (sum % 4
+    == 2 with an even quotient), so widths that are not a multiple of the vector step exercise both."""
+    rng = np.random.default_rng(simd)
+    for h, w in ((94, 310), (50, 38), (12, 12), (2, 18)):
+        src = rng.integers(0, 256, (2 * h, 2 * w)).astype(np.uint8)
+        got = O.resize(src, w, h, simd)
+        assert np.array_equal(got, _area2_py(src, simd)), (h, w)
+    # an odd source width is not an exact 2x step: the linear path (1241 -> 620)
+    src = rng.integers(0, 256, (376, 1241)).astype(np.uint8)
+    assert np.array_equal(O.resize(src, 620, 188, simd), _resize_py(src, 620, 188, simd))
+
+
+def test_reference_refused_geometries():
+    """levels of 19 px or less are taken (square images: nIni = 1 on every level); a level
+    lower than 32 px but wider makes the reference's DistributeOctTree throw (vpIniNodes.resize(nIni < 0)) and
+    the oracle refuses it as ValueError, as pybind11 raises the reference's std::length_error."""
+    img = synth.make_pair(3, 128, 128)[0]
+    ex = O.OracleExtractor(nfeatures=300, scaleFactor=1.2, nlevels=12)
+    kps, desc = ex.extract(img)
+    assert len(kps) > 0 and min(p.shape[0] for p in ex.pyramid()) <= 19
+    sq = O.OracleExtractor(nfeatures=1000, scaleFactor=2.0, nlevels=6)
+    sq.extract(synth.make_pair(4, 400, 400)[0])
+    assert [p.shape for p in sq.pyramid()] == [(400, 400), (200, 200), (100, 100), (50, 50), (25, 25), (12, 12)]
+    for (h, w), prm in (((96, 160), dict(nlevels=12)), ((376, 1241), dict(scaleFactor=2.0, nlevels=8))):
+        with pytest.raises(ValueError):
+            O.OracleExtractor(**prm).extract(synth.make_pair(5, w, h)[0])
+    assert len(O.OracleExtractor(scaleFactor=2.0, nlevels=4).extract(synth.make_pair(5)[0])[0]) > 0
