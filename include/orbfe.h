@@ -32,7 +32,9 @@ extern "C" {
 /* ABI revision of this header (orbfe_abi_version() returns the library's).  4: ORBFE_NSTAGES = 5 (stage 3
  * describe, 4 stereo; the round-1 blur stage and orbfe_set_blur_fork are gone), orbfe_set_graphs,
  * orbfe_set_octree_kernel / orbfe_get_octree_kernel, orbfe_debug_detect_stats. */
-#define ORBFE_ABI_VERSION 4
+#define ORBFE_ABI_VERSION 5
+/* frames whose sheared pyramids the lazy frame path (want_pyramid = 2) keeps on the device */
+#define ORBFE_FRAME_RING 8
 int32_t orbfe_abi_version(void);
 
 #define ORBFE_OK 0
@@ -130,7 +132,10 @@ int orbfe_stereo_match(orbfe_handle hl, orbfe_handle hr, double bf, float fx, fl
  * every result copied into page-locked host memory before a single synchronisation.  The fetch calls
  * below then only copy host memory.  Both images are width x height u8 with row stride `stride`; an
  * empty image (width or height 0) yields no keypoints (ORBextractor.cpp:1045-1046).  bf / fx as in
- * orbfe_stereo_match. */
+ * orbfe_stereo_match.  want_pyramid: 0 none (orbfe_frame_pyramid builds them on request), 1 the sheared
+ * views copied into the frame buffer with the results, 2 lazy: the views stay in a device ring of
+ * ORBFE_FRAME_RING frames and cross PCIe only when orbfe_frame_pyramid_fetch asks for them (Frame.py:59-60
+ * keeps the lists, but the tracking loop rarely reads them). */
 int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* right, int32_t width, int32_t height,
                         int32_t stride, double bf, float fx, int32_t want_pyramid);
 /* keypoints / descriptors of side 0 (left) or 1 (right) of the last frame (operator_kd's outputs) */
@@ -142,6 +147,13 @@ int orbfe_frame_fetch_stereo(orbfe_handle h, float* u_right, float* depth, int8_
  * orbfe_pyramid).  Built at extraction when want_pyramid was set, otherwise now.  out = NULL queries
  * the size. */
 int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* out, int32_t* w_out, int32_t* h_out);
+/* serial number of the last frame (1, 2, ...) and the oldest serial the ring can still hold (a frame extracted
+ * with want_pyramid != 2, or before a geometry change, is not in it) */
+int orbfe_frame_serial(orbfe_handle h, int64_t* serial, int64_t* oldest);
+/* both sheared pyramids' bytes of side 0 / 1 of frame `serial` (extracted with want_pyramid = 2): every
+ * level's w_l x h_l view at its shear offset (levels concatenated, 4-byte aligned; bytes = the geometry's
+ * shear size, orbfe_batch_view_get).  ORBFE_ESTATE once ORBFE_FRAME_RING newer frames have replaced it. */
+int orbfe_frame_pyramid_fetch(orbfe_handle h, int64_t serial, int32_t side, uint8_t* out, int64_t bytes);
 
 /* cv::undistortPoints(pts, K, D, noArray(), K) as Frame.undistort_keypoints (Frame.py:306) and
  * Tracking.compute_image_bounds (Tracking.py:132) call it: OpenCV 4.x's 5-iteration fixed point in double

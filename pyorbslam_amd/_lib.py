@@ -61,6 +61,8 @@ SIGNATURES = {
     "orbfe_frame_fetch_stereo": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                  C.POINTER(C.c_int32)],
     "orbfe_frame_pyramid": [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
+    "orbfe_frame_serial": [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
+    "orbfe_frame_pyramid_fetch": [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64],
     "orbfe_undistort_points": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
                                C.c_void_p],
     "orbfe_png_decode": [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],

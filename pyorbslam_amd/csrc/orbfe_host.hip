@@ -38,6 +38,8 @@ inline short sat_short(int v) { return (short)std::min(std::max(v, -32768), 3276
 
 // concurrent chunks of orbfe_frontend_batch_device (the box exposes 4 hardware queues per process)
 constexpr int kLanes = 4;
+// frames whose sheared pyramids the lazy frame path keeps on the device (include/orbfe.h ORBFE_FRAME_RING)
+constexpr int kFrameRing = ORBFE_FRAME_RING;
 // profiling events per batch: stage k (resize, detect, octree, describe, stereo) spans events k -> k + 1;
 // see prof_mark
 constexpr int kProfEvents = ORBFE_NSTAGES + 1;
@@ -134,6 +136,13 @@ struct orbfe_ctx {
     // per-frame stereo path (orbfe_frame_extract): both images staged in d_in (pitch frame_pitch), the
     // sheared pyramids in d_shear, every result copied into the pinned h_frame before one synchronisation
     DevBuf<uint8_t> d_shear;
+    // want_pyramid == 2 (lazy): every frame's two sheared views stay in a device ring of kFrameRing slots
+    // (frame serial s in slot s % kFrameRing) and reach the host only when fetched
+    // (orbfe_frame_pyramid_fetch), while the serial is still in the ring
+    DevBuf<uint8_t> d_ring;
+    int64_t frame_serial = 0;                  // the last frame's serial (1, 2, ...)
+    int64_t ring_serial[kFrameRing] = {};      // the serial whose views each slot holds (0: none)
+    bool frame_ring = false;                   // the last frame put its views in the ring
     DevBuf<float> d_uin, d_uout;  // orbfe_undistort_points scratch
     HostBuf<uint8_t> h_frame;
     HostBuf<uint8_t> h_in;  // pinned staging of host images (a pageable 2-D copy goes row by row)
@@ -613,6 +622,7 @@ void reserve(orbfe_ctx& c, int W, int H, int max_images) {
         invalidate_results(c);
         c.drop_graphs();
         c.cascades.clear();
+        for (int64_t& r : c.ring_serial) r = 0;  // no earlier frame's views survive a geometry change
         build_geometry(c, W, H);
         c.max_images = 0;
         c.d_cells.ensure(c.cells.size());
@@ -1161,10 +1171,19 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
             h->have_frame = true;
             return;
         }
+        if (want_pyramid < 0 || want_pyramid > 2) throw Error(ORBFE_EINVAL, "want_pyramid must be 0, 1 or 2");
+        const bool lazy = want_pyramid == 2;
+        if (lazy) want_pyramid = 0;  // the views go to the ring below, not into the frame buffer
         hipStream_t s = own(*h);
         const int64_t pitch = ((int64_t)width * height + 255) & ~(int64_t)255;
         h->d_in.ensure(2 * (size_t)pitch);
         if (want_pyramid) h->d_shear.ensure(2 * (size_t)g.shear_bytes);
+        if (lazy) {
+            const uint8_t* before = h->d_ring.p;
+            h->d_ring.ensure((size_t)kFrameRing * 2 * (size_t)g.shear_bytes);
+            if (h->d_ring.p != before)
+                for (int64_t& r : h->ring_serial) r = 0;
+        }
         const uint8_t* pair[2] = {left, right};
         stage_host(*h, pair, 2, width, height, stride, pitch);
         uint8_t* hb_dev = nullptr;  // the frame buffer as the device addresses it (k_copy_segments writes it)
@@ -1199,6 +1218,14 @@ int orbfe_frame_extract(orbfe_handle h, const uint8_t* left, const uint8_t* righ
             if (want_pyramid) seg(h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes);
             HIPCK(launch_copy_segments(cp, q));
         });
+        const int64_t serial = ++h->frame_serial;
+        h->ring_serial[serial % kFrameRing] = 0;
+        if (lazy) {  // both views into this serial's ring slot, behind the graph (one graph for every slot)
+            HIPCK(launch_shear(g, h->d_in.p, pitch, h->d_ws.p,
+                               h->d_ring.p + (size_t)(serial % kFrameRing) * 2 * (size_t)g.shear_bytes, 2, s));
+            h->ring_serial[serial % kFrameRing] = serial;
+        }
+        h->frame_ring = lazy;
         HIPCK(hipStreamSynchronize(s));
         h->last_in = h->d_in.p;
         h->last_pitch = h->frame_pitch = pitch;
@@ -1259,16 +1286,45 @@ int orbfe_frame_pyramid(orbfe_handle h, int32_t side, int32_t level, uint8_t* ou
         if (w_out) *w_out = L.w;
         if (h_out) *h_out = L.h;
         if (!out) return;
-        if (!h->frame_pyr) {  // not requested at extraction: build and fetch both views now
+        if (!h->frame_pyr) {  // not requested at extraction: build (or take from the ring) and fetch both views now
             hipStream_t s = own(*h);
-            h->d_shear.ensure(2 * (size_t)g.shear_bytes);
-            HIPCK(launch_shear(g, h->d_in.p, h->frame_pitch, h->d_ws.p, h->d_shear.p, 2, s));
-            HIPCK(hipMemcpyAsync(h->h_frame.p + h->fo_shear, h->d_shear.p, 2 * (size_t)g.shear_bytes,
-                                 hipMemcpyDeviceToHost, s));
+            const uint8_t* src;
+            if (h->frame_ring) {
+                src = h->d_ring.p + (size_t)(h->frame_serial % kFrameRing) * 2 * (size_t)g.shear_bytes;
+            } else {
+                h->d_shear.ensure(2 * (size_t)g.shear_bytes);
+                HIPCK(launch_shear(g, h->d_in.p, h->frame_pitch, h->d_ws.p, h->d_shear.p, 2, s));
+                src = h->d_shear.p;
+            }
+            HIPCK(hipMemcpyAsync(h->h_frame.p + h->fo_shear, src, 2 * (size_t)g.shear_bytes, hipMemcpyDeviceToHost, s));
             HIPCK(hipStreamSynchronize(s));
             h->frame_pyr = true;
         }
         std::memcpy(out, h->h_frame.p + h->fo_shear + side * (size_t)g.shear_bytes + L.shear_off, (size_t)L.w * L.h);
+    });
+}
+
+int orbfe_frame_serial(orbfe_handle h, int64_t* serial, int64_t* oldest) {
+    return guarded([&] {
+        if (!h || !serial) throw Error(ORBFE_EINVAL, "null argument");
+        *serial = h->frame_serial;
+        if (oldest) *oldest = std::max<int64_t>(1, h->frame_serial - kFrameRing + 1);
+    });
+}
+
+int orbfe_frame_pyramid_fetch(orbfe_handle h, int64_t serial, int32_t side, uint8_t* out, int64_t bytes) {
+    return guarded([&] {
+        if (!h || !out) throw Error(ORBFE_EINVAL, "null argument");
+        if (side != 0 && side != 1) throw Error(ORBFE_EINVAL, "side must be 0 (left) or 1 (right)");
+        const Geo& g = h->geo;
+        if (bytes != g.shear_bytes) throw Error(ORBFE_EINVAL, "out must hold the frame geometry's shear_bytes");
+        if (serial < 1 || h->ring_serial[serial % kFrameRing] != serial)
+            throw Error(ORBFE_ESTATE, "that frame's pyramid has left the device ring (fetch it before " +
+                                          std::to_string(kFrameRing) + " newer frames)");
+        hipStream_t s = own(*h);
+        HIPCK(hipMemcpyAsync(out, h->d_ring.p + ((size_t)(serial % kFrameRing) * 2 + side) * (size_t)g.shear_bytes,
+                             (size_t)g.shear_bytes, hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
     });
 }
 

@@ -22,7 +22,7 @@ from itertools import starmap
 import numpy as np
 
 from ._lib import call, ptr, pyhost
-from .pyORBExtractor import ORBextractor, keypoint_tuples
+from .pyORBExtractor import LazyPyramid, ORBextractor, keypoint_tuples
 
 
 def stereo_match_arrays(left: ORBextractor, right: ORBextractor, mbf: float, fx32) -> dict:
@@ -124,6 +124,12 @@ _CTOR_ARG_ATTRS = ("frame_args", "fx", "fy", "cx", "cy", "invfx", "invfy", "mfGr
                    "mThDepth", "mpORBextractorLeft", "mpORBextractorRight")
 
 
+def _copy_pyramid(pyr):
+    if isinstance(pyr, LazyPyramid):
+        return pyr.copy()
+    return [p.copy() for p in pyr]
+
+
 def frame_copy(self, frame):
     """Frame.copy (Frame.py:75-112) without its re-extraction.
 
@@ -143,8 +149,9 @@ def frame_copy(self, frame):
     new.mb = new.mbf / new.mK[0][0]
     new.mvKeys_ = list(self.mvKeys_)
     new.mvKeysRight_ = list(self.mvKeysRight_)
-    new.mvImagePyramidLeft = [p.copy() for p in self.mvImagePyramidLeft]
-    new.mvImagePyramidRight = [p.copy() for p in self.mvImagePyramidRight]
+    # (a lazy frame's lists copy lazily: LazyPyramid.copy moves nothing while the views are on the device)
+    new.mvImagePyramidLeft = _copy_pyramid(self.mvImagePyramidLeft)
+    new.mvImagePyramidRight = _copy_pyramid(self.mvImagePyramidRight)
     cls.nNextId += 1
     # the reference's overrides (Frame.py:78-110)
     new.mpORBvocabulary = frame.mpORBvocabulary

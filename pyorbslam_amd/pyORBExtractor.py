@@ -10,11 +10,73 @@ All pixel work runs in the gfx950 library (liborbfe.so); there is no CPU path.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
+from collections.abc import Sequence
 
 import numpy as np
 
 from . import _lib
 from ._lib import KP_DTYPE, call, ptr
+
+
+FRAME_RING = 8  # include/orbfe.h ORBFE_FRAME_RING: frames whose sheared views stay on the device
+
+
+class LazyPyramid(Sequence):
+    """GetImagePyramid() after a lazy frame (operator_kd_stereo with want_pyramid=True): the reference's list
+    of sheared uint8 views (opencv_type_casters.h:232-239), fetched from the device ring the first time an
+    element is read (index, iteration, comparison, copy) — Frame.__init__ stores both lists (Frame.py:59-60)
+    but the tracking loop reads them only in the reference's own compute_stereo_matches, which the GPU path
+    replaces.  Before ORBFE_FRAME_RING newer frames of its extractor evict the views, a list still alive is
+    fetched.  Indexing and len() behave as on the list; the type is not `list` (a list subclass could be read
+    by CPython's fast paths without filling)."""
+
+    __slots__ = ("_src", "_levels", "__weakref__")
+
+    def __init__(self, owner, side: int, serial: int):
+        self._src = (owner, side, serial)
+        self._levels = None
+        owner._lazy.append((serial, weakref.ref(self)))
+
+    def _fill(self) -> list:
+        if self._levels is None:
+            owner, side, serial = self._src
+            self._levels = owner._fetch_ring(side, serial)
+            self._src = None
+        return self._levels
+
+    @property
+    def filled(self) -> bool:
+        return self._levels is not None
+
+    def __len__(self) -> int:
+        return len(self._levels) if self._levels is not None else self._src[0]._nlevels
+
+    def __getitem__(self, i):
+        return self._fill()[i]
+
+    def __iter__(self):
+        return iter(self._fill())
+
+    def __eq__(self, other):
+        return list(self) == (list(other) if isinstance(other, (LazyPyramid, list)) else other)
+
+    def __add__(self, other):
+        return list(self) + list(other)
+
+    def __radd__(self, other):
+        return list(other) + list(self)
+
+    def copy(self):
+        """Another lazy list of the same views while they are on the device (Frame.copy keeps the pyramids
+        without moving them); a list of copied arrays once fetched."""
+        if self._levels is None:
+            owner, side, serial = self._src
+            return LazyPyramid(owner, side, serial)
+        return [a.copy() for a in self._levels]
+
+    def __repr__(self) -> str:
+        return repr(self._fill())
 
 
 class ORBextractor:
@@ -44,6 +106,10 @@ class ORBextractor:
         self._pyr_src = None
         self._pyr_cache = None
         self._dependents = []
+        # lazy frames (want_pyramid=True): (serial, weakref) of every LazyPyramid handed out, and the
+        # extractors whose pyramid is a frame of this handle still in the device ring
+        self._lazy = []
+        self._ring_dependents = []
         self.stereo_result = None
         self._pending_image = None
 
@@ -89,16 +155,12 @@ class ORBextractor:
                 raise RuntimeError("GetImagePyramid(sheared=False) is not available after operator_kd_stereo")
             return [a.copy() for a in self._pyr_cache]
         out = []
+        if self._pyr_src is not None and sheared and self._pyr_src[3]:  # a lazy frame: views in the device ring
+            owner, side, serial, _ = self._pyr_src
+            return LazyPyramid(owner, side, serial)
         if self._pyr_src is not None and sheared:  # the frame path: every level out of one allocation
-            owner, side = self._pyr_src
-            shapes = owner._frame_shapes
-            if shapes is None:  # level sizes of the owner's frame geometry (cleared by the next frame)
-                shapes = []
-                for l in range(self._nlevels):
-                    w, h = C.c_int32(), C.c_int32()
-                    call("orbfe_frame_pyramid", owner.handle, side, l, None, C.byref(w), C.byref(h))
-                    shapes.append((h.value, w.value))
-                owner._frame_shapes = shapes
+            owner, side = self._pyr_src[:2]
+            shapes = owner._level_shapes(side)
             buf = np.empty(sum(hh * ww for hh, ww in shapes), np.uint8)
             o = 0
             for l, (hh, ww) in enumerate(shapes):
@@ -116,6 +178,56 @@ class ORBextractor:
             call("orbfe_pyramid", self._h, l, ptr(a), int(sheared), C.byref(w), C.byref(h))
             out.append(a)
         return out
+
+    def _level_shapes(self, side: int) -> list:
+        """(h, w) of every level of this handle's frame geometry (cleared by a frame of another size)."""
+        shapes = self._frame_shapes
+        if shapes is None:
+            shapes = []
+            for l in range(self._nlevels):
+                w, h = C.c_int32(), C.c_int32()
+                call("orbfe_frame_pyramid", self._h, side, l, None, C.byref(w), C.byref(h))
+                shapes.append((h.value, w.value))
+            self._frame_shapes = shapes
+        return shapes
+
+    def _fetch_ring(self, side: int, serial: int) -> list:
+        """Side `side`'s sheared views of this handle's frame `serial` from the device ring: one transfer into
+        one allocation, the levels at their 4-byte aligned offsets (orbfe_frame_pyramid_fetch)."""
+        shapes = self._level_shapes(side)
+        offs, o = [], 0
+        for hh, ww in shapes:
+            offs.append(o)
+            o += (hh * ww + 3) & ~3
+        buf = np.empty(max(o, 1), np.uint8)
+        call("orbfe_frame_pyramid_fetch", self._h, int(serial), int(side), ptr(buf), o)
+        return [buf[a:a + hh * ww].reshape(hh, ww) for a, (hh, ww) in zip(offs, shapes)]
+
+    def _evict_ring(self, next_serial: int) -> None:
+        """Before frame `next_serial` replaces ring slot next_serial % FRAME_RING: fetch every lazy pyramid
+        still alive and unread whose frame would leave the ring, and give the extractors still reading such a
+        frame a host copy."""
+        keep = []
+        for serial, ref in self._lazy:
+            lp = ref()
+            if lp is None or lp.filled:
+                continue
+            if serial <= next_serial - FRAME_RING:
+                lp._fill()
+            else:
+                keep.append((serial, ref))
+        self._lazy = keep
+        deps = []
+        for ex in self._ring_dependents:
+            src = ex._pyr_src
+            if src is None or src[0] is not self or not src[3]:
+                continue
+            if src[2] <= next_serial - FRAME_RING:
+                ex._pyr_cache = self._fetch_ring(src[1], src[2]) if ex._extracted else None
+                ex._pyr_src = None
+            else:
+                deps.append(ex)
+        self._ring_dependents = deps
 
     # ---- operator_kd (orb_extractor.cpp:31-38, ORBextractor.cpp:1042-1104) -----------------------------
     def operator_kd(self, image):
@@ -145,6 +257,9 @@ class ORBextractor:
             if ex._pyr_src is not None and ex._pyr_src[0] is self:
                 if ex is replaced:
                     ex._extracted = False
+                elif ex._pyr_src[3]:  # a lazy frame: its views stay in the device ring (_evict_ring)
+                    self._ring_dependents.append(ex)
+                    continue
                 else:
                     ex._pyr_cache = ex.GetImagePyramid() if ex._extracted else None
                 ex._pyr_src = None
@@ -159,6 +274,8 @@ class ORBextractor:
         desc = np.empty((cap, 32), np.uint8)
         n = C.c_int32()
         self._release_frame()
+        if self._frame_hw is not None and (h, w) != self._frame_hw and h and w:
+            self._evict_ring(2 ** 62)  # another geometry clears the ring (reserve): read every lazy list first
         self._pyr_src = None
         self._pyr_cache = None
         self.stereo_result = None
@@ -187,9 +304,19 @@ class ORBextractor:
         h, w = L.shape
         self._release_frame(replaced=right_extractor)
         if (h, w) != self._frame_hw:
+            # a new geometry: the ring's frames are gone (reserve), so every lazy list still unread is read now
+            self._evict_ring(2 ** 62)
             self._frame_hw, self._frame_shapes = (h, w), None
+        else:
+            serial = C.c_int64()
+            call("orbfe_frame_serial", self._h, C.byref(serial), None)
+            self._evict_ring(serial.value + 1)
+        # want_pyramid: the sheared views stay on the device until read (2, lazy); False: built on request
         call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
-             int(bool(want_pyramid)))
+             2 if want_pyramid else 0)
+        serial = C.c_int64()
+        call("orbfe_frame_serial", self._h, C.byref(serial), None)
+        lazy = bool(want_pyramid)
         out = []
         for side, ex in ((0, self), (1, right_extractor)):
             n = C.c_int32()  # the count first (no copy), then the records straight into exact-size arrays
@@ -198,7 +325,7 @@ class ORBextractor:
             desc = np.empty((n.value, 32), np.uint8)
             call("orbfe_frame_fetch", self._h, side, ptr(kps), ptr(desc), n.value, C.byref(n))
             ex._set_result(kps, desc, n.value, w > 0 and h > 0, exact=True)
-            ex._pyr_src = (self, side) if w > 0 and h > 0 else None
+            ex._pyr_src = (self, side, serial.value, lazy) if w > 0 and h > 0 else None
             ex._pyr_cache = None
             ex.stereo_result = None
             out += [ex._kps, ex._desc]

@@ -109,7 +109,7 @@ def test_graph_frame_path_equals_stream_path():
             assert np.array_equal(x, y)
     cap, lau = C.c_int64(), C.c_int64()
     call("orbfe_graph_stats", a.handle, C.byref(cap), C.byref(lau), None)
-    assert cap.value == 2 and lau.value == 4  # one graph per want_pyramid value
+    assert cap.value == 1 and lau.value == 4  # lazy pyramids (k_shear behind the graph) or none: one graph
     kl, dl = O.OracleExtractor(**KITTI).extract(seq.frame(3)[0])
     assert ga[0].tobytes() == kl.tobytes() and np.array_equal(ga[1], dl)
 

@@ -417,3 +417,39 @@ def test_right_extractor_keeps_its_pyramid_after_the_left_moves_on():
     o.extract(R2)
     for g_, w_ in zip(rB.GetImagePyramid(), o.sheared_pyramid()):
         assert np.array_equal(g_, w_)
+
+
+def test_lazy_frame_pyramids_ring():
+    """the frame path's sheared pyramids stay in a device ring (ORBFE_FRAME_RING frames) and
+    cross PCIe only when read.  Lists read late, copied lazily (Frame.copy) or forced out by the ring's
+    eviction all equal the oracle's views of their own frame; unread lists of dropped frames cost nothing."""
+    from oracle.oracle import OracleExtractor
+    from pyorbslam_amd.pyORBExtractor import FRAME_RING, LazyPyramid
+    seq = synth.StereoSequence(1, 1241, 376, 1.0)
+    left, right = ORBextractor(**KITTI), ORBextractor(**KITTI)
+    kept = []
+    for k in range(FRAME_RING + 3):
+        L, R = seq.frame(k)
+        left.operator_kd_stereo(L, R, right, BF, np.float32(FX))
+        pl, pr = left.GetImagePyramid(), right.GetImagePyramid()
+        assert isinstance(pl, LazyPyramid) and not pl.filled and len(pl) == KITTI["nlevels"]
+        kept.append((k, pl, pr.copy()))
+        if 1 <= k <= FRAME_RING:
+            assert not kept[1][1].filled  # frame 1's lists are still on the device ...
+    # ... frames 0 .. 2 left the ring while their lists were alive: fetched at eviction
+    assert all(kept[k][1].filled and kept[k][2].filled for k in range(3))
+    assert not any(kept[k][1].filled or kept[k][2].filled for k in range(3, FRAME_RING + 3))
+    o = OracleExtractor(**KITTI)
+    for k in (0, 2, 3, FRAME_RING + 2):
+        L, R = seq.frame(k)
+        o.extract(L)
+        assert all(np.array_equal(a, b) for a, b in zip(kept[k][1], o.sheared_pyramid())), f"left, frame {k}"
+        o.extract(R)
+        assert all(np.array_equal(a, b) for a, b in zip(kept[k][2], o.sheared_pyramid())), f"right, frame {k}"
+    # the extractors' own GetImagePyramid of the last frame, and the eager path (built on request)
+    last_r = right.GetImagePyramid()
+    assert all(np.array_equal(a, b) for a, b in zip(last_r, o.sheared_pyramid()))
+    L, R = seq.frame(FRAME_RING + 2)
+    left.operator_kd_stereo(L, R, right, BF, np.float32(FX), want_pyramid=False)
+    eager = right.GetImagePyramid()
+    assert isinstance(eager, list) and all(np.array_equal(a, b) for a, b in zip(eager, o.sheared_pyramid()))
