@@ -727,7 +727,7 @@ std::unique_ptr<orbfe_ctx::Cascade> resize_strips(const orbfe_ctx& c, int S) {
     cs->S = S;
     cs->off_b = (int)a16(A);
     cs->off_x = cs->off_b + (int)a16(B);
-    cs->lds = cs->off_x + (int)((size_t)g.rs_ngrp * 36);
+    cs->lds = cs->off_x + (int)((size_t)g.rs_ngrp * 72);  // two levels' x entries (k_resize_cascade prefetch)
     if (cs->lds > 150 * 1024) return nullptr;
     cs->tab.ensure(tab.size());
     HIPCK(hipMemcpy(cs->tab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));

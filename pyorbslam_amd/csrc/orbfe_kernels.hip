@@ -498,8 +498,42 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
     const int16_t* st = tab + (int64_t)strip * L * 4;
     const uint32_t baseA = (uint32_t)(uintptr_t)(lds_u32*)rs_lds;
     const uint32_t baseB = baseA + (uint32_t)offB;
-    uint4* s_xa = (uint4*)(rs_lds + offX);  // per group: v_perm selectors, then (a0, a1) weights
-    int* s_sx0 = (int*)(s_xa + 2 * g.rs_ngrp);  // per group: its first source column
+    // per group: v_perm selectors, then (a0, a1) weights; its first source column — double-buffered by level
+    // parity: level l + 1's entries are loaded into registers while level l computes
+    uint4* s_xa2[2] = {(uint4*)(rs_lds + offX), (uint4*)(rs_lds + offX) + 2 * g.rs_ngrp};
+    int* s_sx2[2] = {(int*)(s_xa2[1] + 2 * g.rs_ngrp), (int*)(s_xa2[1] + 2 * g.rs_ngrp) + g.rs_ngrp};
+    constexpr int kPre = 2;  // groups per thread held in registers (512 threads: levels up to 4 096 px)
+    uint4 pq0[kPre], pq1[kPre];
+    auto prefetch = [&](int l) {
+        if (l >= g.nlevels) return;
+        const uint4* xg = (const uint4*)(xt + g.lv[l].xtab_off);
+        const int ng = (g.lv[l].w + 3) >> 2;
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) {
+            const int gi = t + 512 * k;
+            if (gi < ng) {
+                pq0[k] = xg[2 * gi];
+                pq1[k] = xg[2 * gi + 1];
+            }
+        }
+    };
+    auto commit = [&](int l) {
+        uint4* sxa = s_xa2[l & 1];
+        int* ssx = s_sx2[l & 1];
+        const int ng = (g.lv[l].w + 3) >> 2;
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) {
+            const int gi = t + 512 * k;
+            if (gi < ng) {
+                const uint4 q0 = pq0[k], q1 = pq1[k];
+                auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
+                sxa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+                sxa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
+                ssx[gi] = (int)q0.x;
+            }
+        }
+    };
+    prefetch(1);
     // ---- level 0 rows the strip's level 1 needs, staged as a flat dword run (k_resize_rows' staging)
     uint32_t src_base = baseA, src_sh;
     int src_row0, src_stride;
@@ -533,15 +567,11 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
         const LevelGeo& Lv = g.lv[l];
         const int c0 = st[4 * l], c1 = st[4 * l + 1], o0 = st[4 * l + 2], o1 = st[4 * l + 3];
         const int ngrp = (Lv.w + 3) >> 2, nch = (ngrp + 63) >> 6;
-        // x selectors / weights of the level (k_resize's per-group form)
-        const uint4* xg = (const uint4*)(xt + Lv.xtab_off);
-        for (int gi = t; gi < ngrp; gi += blockDim.x) {
-            const uint4 q0 = xg[2 * gi], q1 = xg[2 * gi + 1];
-            auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
-            s_xa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
-            s_xa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
-            s_sx0[gi] = (int)q0.x;
-        }
+        // x selectors / weights of the level (k_resize's per-group form), loaded during the previous level
+        commit(l);
+        prefetch(l + 1);
+        const uint4* s_xa = s_xa2[l & 1];
+        const int* s_sx0 = s_sx2[l & 1];
         const uint32_t dst_base = (l & 1) ? baseB : baseA;
         __syncthreads();  // selectors staged; the source rows complete (previous level / staging)
         const ResizeY* yb = yt + Lv.ytab_off;
@@ -1848,29 +1878,32 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     // Every key once: keys k = tid, tid + nthr, ... (consecutive keys in consecutive lanes: coalesced slot
     // reads), kObBatch of them in flight per thread; a key's cell is the cell of its 64-key block's first key
     // (bcell) walked forward over the few cells the block spans.  fn(k, slot value, code) for k < K.
+    // the 1 024-thread (small-batch) form keeps twice as many loads in flight: a level-0 workgroup holds ~5 000
+    // keys, i.e. ~5 per thread, which then take one round trip instead of two
+    constexpr int OB = NT >= 1024 ? 2 * kObBatch : kObBatch;
     auto for_keys = [&](int tid, int nthr, auto&& fn) {
-        for (int k0 = tid; k0 < K; k0 += nthr * kObBatch) {
-            int lo[kObBatch];
+        for (int k0 = tid; k0 < K; k0 += nthr * OB) {
+            int lo[OB];
 #pragma unroll
-            for (int u = 0; u < kObBatch; ++u) lo[u] = d.bcell[min(min(k0 + nthr * u, K - 1) >> 6, nblk - 1)];
+            for (int u = 0; u < OB; ++u) lo[u] = d.bcell[min(min(k0 + nthr * u, K - 1) >> 6, nblk - 1)];
             bool more = true;
             while (__ballot(more)) {
                 more = false;
 #pragma unroll
-                for (int u = 0; u < kObBatch; ++u) {
+                for (int u = 0; u < OB; ++u) {
                     const bool f = d.coff[lo[u] + 1] <= k0 + nthr * u && k0 + nthr * u < K;
                     lo[u] += f;
                     more |= f;
                 }
             }
-            uint32_t v[kObBatch];
+            uint32_t v[OB];
 #pragma unroll
-            for (int u = 0; u < kObBatch; ++u) {
+            for (int u = 0; u < OB; ++u) {
                 const int k = k0 + nthr * u;
                 v[u] = k < K ? islots[d.soff[lo[u]] + (k - d.coff[lo[u]])] : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < kObBatch; ++u) fn(k0 + nthr * u, v[u], key_code(v[u]));
+            for (int u = 0; u < OB; ++u) fn(k0 + nthr * u, v[u], key_code(v[u]));
         }
     };
     // the first sweep also leaves every key's slot value in key order in global scratch (kc, the level's
