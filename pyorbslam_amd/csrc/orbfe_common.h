@@ -40,6 +40,8 @@ struct LevelGeo {
     int xtab_off, ytab_off;
     int xmax;            // first column whose sx+1 >= src width
     int xvec;            // end of OpenCV's vectorised span of the vertical pass
+    int wide;            // 1: a group's 4th pixel lies past its first 8 source bytes (steps near 2): its taps
+                         // come from a window of its own (sx3 - sx0 <= 15; the other pixels' within 8 bytes)
     int area;            // 1: an exact 2x step, cv::resize's INTER_AREA fast path (resizeAreaFast_): the tables
                          // hold the 2x2 average (weights 1024), xvec its vector span, the tail rounds half to even
     // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;

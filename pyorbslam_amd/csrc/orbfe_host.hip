@@ -234,6 +234,7 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
     Lg.xtab_off = (int)xt.size();
     Lg.ytab_off = (int)yt.size();
     Lg.area = 0;
+    Lg.wide = 0;
     if (area_fast && isx == 2 && isy == 2) {
         // cv::resize turns INTER_LINEAR with an exact 2x step into INTER_AREA, whose fast path
         // (resizeAreaFast_, ResizeAreaFastVec_SIMD_8u) averages 2 x 2 blocks: (a + b + c + d + 2) >> 2 over the
@@ -268,11 +269,15 @@ void resize_tables(int sw, int sh, int dw, int dh, int simd, LevelGeo& Lg, std::
     Lg.xmax = xmax;
     // over-read guard of the last group: the last column at weight 2048 (kept inside its group's byte window)
     for (int k = 0; k < 4; ++k) xt.push_back(ResizeX{sw - 1, 2048, 0});
-    // k_resize gathers a 4-pixel group's taps from 8 bytes starting at the group's first sx
-    for (int g0 = Lg.xtab_off; g0 < (int)xt.size() - 4; g0 += 4)
+    // k_resize gathers a 4-pixel group's taps from 8 bytes starting at the group's first sx; with steps near 2
+    // (e.g. 1241 -> 620 at scaleFactor 2) the 4th pixel can fall past them: such a level is `wide` and takes
+    // that pixel's taps from a window of its own (resize_tap3)
+    for (int g0 = Lg.xtab_off; g0 < (int)xt.size() - 4; g0 += 4) {
         for (int k = 1; k < 4; ++k)
-            if (xt[g0 + k].sx - xt[g0].sx < 0 || xt[g0 + k].sx - xt[g0].sx > 6)
-                throw Error(ORBFE_EINVAL, "resize step too large for k_resize's 8-byte tap window");
+            if (xt[g0 + k].sx - xt[g0].sx < 0 || xt[g0 + k].sx - xt[g0].sx > (k == 3 ? 15 : 6))
+                throw Error(ORBFE_EINVAL, "resize step too large for k_resize's tap windows (scale factor > ~2.3)");
+        if (xt[g0 + 3].sx - xt[g0].sx > 6) Lg.wide = 1;
+    }
     int xv = 0;
     if (simd > 0) {
         while (xv <= dw - simd) xv += simd;

@@ -207,6 +207,17 @@ __device__ int block_sum(int v, int* red) {
 //  * compute: per group and row, 2 x (3 LDS dwords, 2 v_alignbyte, 4 v_perm + 4 v_dot2_u32_u16) for the
 //    horizontal taps, then OpenCV's vertical rounding; one aligned dword store per 4 output pixels.
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// Horizontal taps of a group's 4th pixel from a window of its own (LevelGeo::wide): A3 = LDS byte address of
+// its source pixel sx3, aa = its (a0, a1) weights.
+__device__ __forceinline__ uint32_t resize_tap3(uint32_t A3, uint32_t aa) {
+    typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+    const uint32_t o = A3 & 3u;
+    lds_c32* w = (lds_c32*)(uintptr_t)(A3 - o);
+    const uint32_t x = __builtin_amdgcn_alignbyte(w[1], w[0], o);
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(x, x, 0x0c010c00u)),
+                                  __builtin_bit_cast(us2, aa), 0u, false);
+}
 constexpr int kRsSlots = 16;  // staged dwords per thread per pass
 
 #ifdef ORBFE_DEV_VARIANTS  // the round-2 item-mapped kernel, for tools/microbench.py (tools/dbg/build_variant.sh)
@@ -376,6 +387,7 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     bool own = false;
     uint4 e{}, aa{};
     int sx0 = 0;
+    uint32_t d3 = 0;  // LevelGeo::wide: the 4th pixel's source column past the group's first
     auto chunk = [&](int c) {
         grp = remwave ? wg * 64 + lane % rem : c * 64 + lane;
         own = remwave ? lane < rstep * rem : grp < ngrp;
@@ -383,6 +395,7 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             const uint4* xg = (const uint4*)(xt + L.xtab_off);
             const uint4 q0 = xg[2 * grp], q1 = xg[2 * grp + 1];
             sx0 = (int)q0.x;
+            d3 = q1.z - q0.x;
             auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
             e = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
             aa = uint4{q0.y, q0.w, q1.y, q1.w};
@@ -432,8 +445,9 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
                                               __builtin_bit_cast(us2, aa.y), 0u, false);
                 h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
                                               __builtin_bit_cast(us2, aa.z), 0u, false);
-                h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
-                                              __builtin_bit_cast(us2, aa.w), 0u, false);
+                h[3] = L.wide ? resize_tap3(A + d3, aa.w)
+                              : __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                                       __builtin_bit_cast(us2, aa.w), 0u, false);
             };
             uint32_t h0[4], h1[4];
             if (reuse && y.sy0 == psy) {
@@ -529,7 +543,7 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
                 auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
                 sxa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
                 sxa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
-                ssx[gi] = (int)q0.x;
+                ssx[gi] = (int)(q0.x | ((q1.z - q0.x) << 24));  // sx0, and the 4th pixel's offset (wide levels)
             }
         }
     };
@@ -586,7 +600,9 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
             const int grp = ch * 64 + lane;
             if (grp < ngrp) {
                 const uint4 e = s_xa[2 * grp], aa = s_xa[2 * grp + 1];
-                const int sx0 = s_sx0[grp];
+                const int sxp = s_sx0[grp];
+                const int sx0 = sxp & 0xFFFFFF;
+                const uint32_t d3 = (uint32_t)sxp >> 24;
                 const ResizeY y = yb[r];
                 const uint32_t lsrc = src_base + src_sh + (uint32_t)sx0;
                 const uint32_t r0 = (uint32_t)((y.sy0 - src_row0) * src_stride), r1 = (uint32_t)((y.sy1 - src_row0) * src_stride);
@@ -602,8 +618,9 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
                                                   __builtin_bit_cast(us2, aa.y), 0u, false);
                     h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
                                                   __builtin_bit_cast(us2, aa.z), 0u, false);
-                    h[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
-                                                  __builtin_bit_cast(us2, aa.w), 0u, false);
+                    h[3] = Lv.wide ? resize_tap3(A + d3, aa.w)
+                                   : __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                                            __builtin_bit_cast(us2, aa.w), 0u, false);
                 };
                 uint32_t h0[4], h1[4];
                 taps(r0, h0);
@@ -2061,6 +2078,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             return (uint64_t)code | ((uint64_t)(((uint32_t)n << 8) | (uint32_t)dp) << 32);
         };
         for (int i = t; i < NC; i += NT) d.proc[i] = 0;  // (ordered before use by bscan's barriers)
+        if (t < 16 * NW) (&s_cw[0][0])[t] = 0;
         // cumulative bin counts, bins[B] = K
         {
             int v[EB];
@@ -2076,6 +2094,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             if (t < 48) (&s_dc[0][0])[t] = 0;
             __syncthreads();
         }
+        mark(40);
         auto cum = [&](int b) { return (int)(d.bins[b] & ~kObDeep); };
         auto ncnt = [&](int dd, int i) {
             const int sh = 2 * (D0 - dd);
@@ -2102,6 +2121,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             }
         }
         __syncthreads();
+        mark(41);
         // the passes the reference makes (:668-672), replayed on the counts: J passes, then finish (1),
         // the careful phase (2), or more full passes below D0 (3)
         int J = 0, mode = 0, S = s_dc[0][0];
@@ -2177,6 +2197,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         int C = s_dc[0][J];
         __syncthreads();
         mark(2);
+        mark(42);
         // children counts of node p of list l (registers: code, depth)
         auto child_counts = [&](uint32_t code, int dp, int p) {
             int4 cc;
@@ -2279,6 +2300,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                 // position ascending), divided until the list reaches N
                 auto cand = [&](int p) { return p < C && node_cnt(cur, p) > 1; };
                 deep_counts(cand);
+                if (iter == 0) mark(43);
                 // candidates in position order -> (size, position | children << 16) at their compacted index
                 int mi[LP], ncl[LP];
                 int mx = 0;
@@ -2308,6 +2330,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                         pa[mi[k]] = p | (ncl[k] << 16);
                     }
                 __syncthreads();
+                if (iter == 0) mark(44);
                 // stable LSD radix sort by size, descending, 4-bit digits while the largest size has any
                 for (int sh = 0; sh < 32 && (s_m[1] >> sh) != 0; sh += 4) {
                     int dg[LP], rk[LP];
@@ -2315,25 +2338,28 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                     for (int k = 0; k < LP; ++k) {
                         const int e = t * LP + k;
                         dg[k] = e < M ? 15 - ((ka[e] >> sh) & 15) : -1;
-                        rk[k] = 0;
                     }
-                    for (int b = 0; b < 16; ++b) {
-                        int acc = 0;
-                        uint64_t mk[LP];
+                    // stable ranks inside the wave: elements (lane, k) in that order; the lanes whose element j
+                    // holds digit x are valid_j & (x's bits of the four digit-bit ballots) — no loop over digits
+                    uint64_t bb[LP][4], vb[LP];
 #pragma unroll
-                        for (int k = 0; k < LP; ++k) mk[k] = __ballot(dg[k] == b);
-                        int below = 0, tot = 0;
+                    for (int k = 0; k < LP; ++k) {
+                        vb[k] = __ballot(dg[k] >= 0);
 #pragma unroll
-                        for (int k = 0; k < LP; ++k) {
-                            below += __popcll(mk[k] & lt);
-                            tot += __popcll(mk[k]);
+                        for (int bit = 0; bit < 4; ++bit) bb[k][bit] = __ballot(dg[k] >= 0 && ((dg[k] >> bit) & 1));
+                    }
+#pragma unroll
+                    for (int k = 0; k < LP; ++k) {
+                        rk[k] = 0;
+                        if (dg[k] < 0) continue;
+#pragma unroll
+                        for (int j = 0; j < LP; ++j) {
+                            uint64_t m = vb[j];
+#pragma unroll
+                            for (int bit = 0; bit < 4; ++bit) m &= ((dg[k] >> bit) & 1) ? bb[j][bit] : ~bb[j][bit];
+                            rk[k] += __popcll(m & lt) + (j < k && dg[j] == dg[k]);
                         }
-#pragma unroll
-                        for (int k = 0; k < LP; ++k) {
-                            if (dg[k] == b) rk[k] = below + acc;
-                            acc += dg[k] == b;
-                        }
-                        if (lane == 0) s_cw[wv][b] = tot;
+                        atomicAdd(&s_cw[wv][dg[k]], 1);
                     }
                     __syncthreads();
                     if (t < 64) {  // offset of (wave w, digit b): every smaller digit, then earlier waves
@@ -2342,6 +2368,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                             for (int w = 0; w < NW; ++w) {
                                 s_co[w][t] = tot;
                                 tot += s_cw[w][t];
+                                s_cw[w][t] = 0;  // for the next pass (its counts come after two barriers)
                             }
                         const int base = wave_incl_scan_dpp(tot) - tot;  // digits below t (lanes >= 16: 0)
                         if (t < 16)
@@ -2359,6 +2386,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                     int* tk = ka; ka = kb; kb = tk;
                     int* tp = pa; pa = pb; pb = tp;
                 }
+                if (iter == 0) mark(45);
                 // growth (children - 1) and children in processing order: a candidate is divided iff the list
                 // before it is below N (:729-730); the divided ones are a prefix
                 int gv[LP];
@@ -2380,6 +2408,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                     }
                 }
                 __syncthreads();
+                if (iter == 0) mark(46);
                 Cn = s_m[3];
                 int kp[LP];
 #pragma unroll
@@ -3759,6 +3788,7 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
         return hipGetLastError();
     }
 #ifdef ORBFE_DEV_VARIANTS
+    if (L.wide) return hipErrorInvalidValue;  // the round-2 kernel gathers every pixel from the group's 8 bytes
     const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
     auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;  // variant 4: k_resize<0>
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
