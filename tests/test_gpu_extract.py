@@ -220,7 +220,7 @@ def test_reference_refused_geometries_gpu():
     """A level lower than 32 px but wider makes the reference's DistributeOctTree throw (vpIniNodes.resize of a
     negative nIni, ORBextractor.cpp:543-550; pybind11 raises std::length_error as ValueError): the drop-in
     raises ValueError for the same geometries, the oracle too."""
-    for (h, w), prm in (((96, 160), dict(nlevels=12)), ((376, 1241), dict(scaleFactor=2.0, nlevels=8))):
+    for (h, w), prm in (((96, 160), dict(KITTI, nlevels=12)), ((376, 1241), dict(KITTI, scaleFactor=2.0))):
         img = synth.make_pair(5, w, h)[0]
         with pytest.raises(ValueError):
             ORBextractor(**prm).extract(img)
