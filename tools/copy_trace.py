@@ -1,7 +1,9 @@
 """Summary of a rocprofv3 --kernel-trace --memory-copy-trace run (tools/host_fed_trace.py): per direction the
 copies' count, bytes, summed duration and GB/s while copying; the span of the traced window; the share of that
 span during which a host->device copy is in flight, during which any kernel runs, and both at once.
-usage: python tools/copy_trace.py TRACE_DIR [--skip-first-s 0.0]"""
+usage: python tools/copy_trace.py TRACE_DIR [--last-h2d 32] [--h2d-bytes 119453696]
+(rocprofv3's memory-copy records carry no size: --h2d-bytes is the host-fed chunk, 128 pairs x 2 x 1241 x 376;
+the window is the last --last-h2d host->device copies, i.e. the timed steps, to the end of the last kernel)"""
 import argparse
 import csv
 import glob
@@ -36,6 +38,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--skip-first-s", type=float, default=0.0)
+    ap.add_argument("--last-h2d", type=int, default=32)
+    ap.add_argument("--h2d-bytes", type=int, default=2 * 128 * 1241 * 376)
     a = ap.parse_args()
     kern, cop = [], []
     for f in glob.glob(f"{a.trace}/**/*kernel_trace.csv", recursive=True):
@@ -47,7 +51,12 @@ def main():
             cop.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), d, int(r.get("Bytes", r.get("Size", 0)))))
     if not kern or not cop:
         raise SystemExit("no kernel or copy records")
-    t0 = min(k[0] for k in kern) + int(a.skip_first_s * 1e9)
+    h2d = sorted(c for c in cop if "HOST_TO_DEVICE" in c[2])
+    if a.last_h2d and len(h2d) >= a.last_h2d:
+        t0 = h2d[-a.last_h2d][0]
+        cop = [(s_, e_, d_, b_ or (a.h2d_bytes if "HOST_TO_DEVICE" in d_ else 0)) for s_, e_, d_, b_ in cop]
+    else:
+        t0 = min(k[0] for k in kern) + int(a.skip_first_s * 1e9)
     kern = [k for k in kern if k[0] >= t0]
     cop = [c for c in cop if c[0] >= t0]
     span = max(max(k[1] for k in kern), max(c[1] for c in cop)) - t0
@@ -55,6 +64,8 @@ def main():
     print(f"window {span / 1e6:.3f} ms, kernel-busy {sum(e - s for s, e in K) / span:.3f} of it")
     for d in sorted({c[2] for c in cop}):
         cs = [c for c in cop if c[2] == d]
+        durs = sorted((c[1] - c[0]) / 1e3 for c in cs)
+        print(f"{d}: per-copy us p50 {durs[len(durs) // 2]:.1f} min {durs[0]:.1f} max {durs[-1]:.1f}")
         U = union([(c[0], c[1]) for c in cs])
         busy = sum(e - s for s, e in U)
         b = sum(c[3] for c in cs)

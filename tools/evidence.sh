@@ -6,10 +6,12 @@
 # standalone pass (--roofline-only) for KITTI and EuRoC: FETCH_SIZE, WRITE_SIZE (profiles/traffic.json via
 # tools/traffic.py), SQ_INSTS_VALU + SQ_INSTS_LDS + GRBM_GUI_ACTIVE, and the busy-cycle group
 # SQ_ACTIVE_INST_VALU + SQ_BUSY_CYCLES + SQ_WAIT_INST_ANY + GRBM_GUI_ACTIVE (profiles/valu.json via tools/valu.py).
-# usage (on the GPU box): bash tools/evidence.sh TAG      -> gpurun_out/ev_TAG/
+# usage (on the GPU box): bash tools/evidence.sh TAG [PART]   -> gpurun_out/ev_TAG/
+#   PART: all (default), a (tests, bench lines, launcher runs, kernel traces), b (PMC passes)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag=${1:-run}
+part=${2:-all}
 out=gpurun_out/ev_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
@@ -22,6 +24,7 @@ step() {  # name, timeout, command...
   tail -n 3 "$out/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
+if [ "$part" != b ]; then
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 step bench 500 python bench.py
 step bench_frame 300 python bench.py --mode frame --steps 96 --warmup 1
@@ -35,6 +38,10 @@ step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt
 step ktrace_share8 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_share8" -o run -- python tools/small_trace.py --pairs 8 --steps 50
 step ktrace_frame 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_frame" -o run -- python tools/small_trace.py --frame --steps 50
 step ktrace_c3 200 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_c3" -o run -- python bench.py --mode frame --steps 96 --warmup 1
+step ktrace_share8x2 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_share8x2" -o run -- python tools/small_trace.py --pairs 8 --steps 50 --graphs 0 --handles 2
+step host_fed_trace 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$out/host_fed_trace" -o run -- python tools/host_fed_trace.py --steps 8
+fi
+[ "$part" = a ] && { echo "evidence done (part a)"; exit 0; }
 for cam in kitti euroc; do
   args="--roofline-only --roofline-steps 2"
   [ $cam = euroc ] && args="$args --width 752 --height 480 --nfeatures 1000"
