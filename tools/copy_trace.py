@@ -1,7 +1,7 @@
 """Summary of a rocprofv3 --kernel-trace --memory-copy-trace run (tools/host_fed_trace.py): per direction the
 copies' count, bytes, summed duration and GB/s while copying; the span of the traced window; the share of that
 span during which a host->device copy is in flight, during which any kernel runs, and both at once.
-usage: python tools/copy_trace.py TRACE_DIR [--last-h2d 32] [--h2d-bytes 119453696]
+usage: python tools/copy_trace.py TRACE_DIR [--last-h2d 32] [--h2d-bytes 119453696] [--d2h-bytes 23670784]
 (rocprofv3's memory-copy records carry no size: --h2d-bytes is the host-fed chunk, 128 pairs x 2 x 1241 x 376;
 the window is the last --last-h2d host->device copies, i.e. the timed steps, to the end of the last kernel)"""
 import argparse
@@ -40,11 +40,14 @@ def main():
     ap.add_argument("--skip-first-s", type=float, default=0.0)
     ap.add_argument("--last-h2d", type=int, default=32)
     ap.add_argument("--h2d-bytes", type=int, default=2 * 128 * 1241 * 376)
+    ap.add_argument("--d2h-bytes", type=int, default=128 * 184928)
     a = ap.parse_args()
-    kern, cop = [], []
+    kern, cop, blit = [], [], []
     for f in glob.glob(f"{a.trace}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            kern.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            iv = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+            # ROCclr moves device->pinned-host copies with a blit kernel: count those as the D2H leg
+            (blit if r["Kernel_Name"].startswith("__amd_rocclr_copy") else kern).append(iv)
     for f in glob.glob(f"{a.trace}/**/*memory_copy_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             d = r.get("Direction", r.get("Kind", "?"))
@@ -61,7 +64,16 @@ def main():
     cop = [c for c in cop if c[0] >= t0]
     span = max(max(k[1] for k in kern), max(c[1] for c in cop)) - t0
     K = union(kern)
-    print(f"window {span / 1e6:.3f} ms, kernel-busy {sum(e - s for s, e in K) / span:.3f} of it")
+    print(f"window {span / 1e6:.3f} ms, kernel-busy (orbfe kernels) {sum(e - s for s, e in K) / span:.3f} of it")
+    blit = [b for b in blit if b[0] >= t0]
+    if blit:
+        B = union(blit)
+        durs = sorted((e - s) / 1e3 for s, e in blit)
+        bb = a.d2h_bytes * len(blit)
+        print(f"blit copy kernels (__amd_rocclr_copyBuffer, the D2H record leg): {len(blit)}, per-kernel us p50 "
+              f"{durs[len(durs) // 2]:.1f}, in flight {sum(e - s for s, e in B) / span:.3f} of the window, "
+              f"{bb / max(sum(e - s for s, e in B), 1):.2f} GB/s while in flight at --d2h-bytes each, "
+              f"overlapping orbfe kernels {inter(B, K) / max(sum(e - s for s, e in B), 1):.3f}")
     for d in sorted({c[2] for c in cop}):
         cs = [c for c in cop if c[2] == d]
         durs = sorted((c[1] - c[0]) / 1e3 for c in cs)
