@@ -68,6 +68,8 @@ def compute_stereo_matches(frame) -> None:
     if res is None or getattr(left, "_stereo_partner", None) is not right:
         res = stereo_match_arrays(left, right, frame.mbf, frame.mK[0][0])
     frame.mvuRight, frame.mvDepth = to_reference_lists(res, left.last_keypoints, frame.mbf)
+    from .matcher import prime_u_right  # the matcher's per-frame mvuRight doubles, from the arrays
+    prime_u_right(frame, res, left.last_keypoints["x"])
 
 
 def _keypoint_cls(frame):

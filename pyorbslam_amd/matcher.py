@@ -330,6 +330,27 @@ def _u_right(frame, with_kinds: bool = False):
     return (ent[1], ent[2]) if with_kinds else ent[1]
 
 
+def prime_u_right(frame, res: dict, xs: np.ndarray) -> None:
+    """Fill _u_right's cache for a frame whose mvuRight list compute_stereo_matches has just built from the
+    stereo arrays (frame.to_reference_lists): the same doubles, from the arrays instead of the 2 000-entry
+    list — u_right widened where status is 1, -1 where 0, float(x) - 0.01 where 2 (Frame.py:273-277)."""
+    vals = frame.mvuRight
+    st = np.asarray(res["status"])
+    if len(vals) != len(st):
+        return
+    arr = np.asarray(res["u_right"], np.float32).astype(np.float64)
+    arr[st == 0] = -1.0
+    z = st == 2
+    if z.any():
+        arr[z] = np.asarray(xs, np.float32)[z].astype(np.float64) - 0.01
+    # np.float32 entries (status 1) are not doubles; -1 (int) and the status-2 Python floats are
+    all_double = not bool(((st != 0) & (st != 2)).any())
+    try:
+        _uright_cache[frame] = ((id(vals), len(vals)), arr, all_double)
+    except TypeError:
+        pass
+
+
 def _blocked(frame):
     """Per slot of the frame: 1 if it holds a map point with observations (ORBMatcher.py's
     `if mvpMapPoints[i]: if mvpMapPoints[i].observations() > 0: continue`)."""

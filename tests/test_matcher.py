@@ -387,3 +387,30 @@ def test_fp_inputs_equal_the_reference_loop():
             return 3.0
 
     assert M2(0.8, True)._f_p_inputs(mps, 1, False) is None
+
+
+def test_prime_u_right_equals_the_list_widening():
+    """frame.compute_stereo_matches primes the matcher's per-frame mvuRight doubles from the stereo arrays;
+    they equal what _u_right computes from the reference's list (same doubles, same all-double flag)."""
+    from pyorbslam_amd import matcher as Mt
+    from pyorbslam_amd.frame import to_reference_lists
+
+    class Fr:
+        pass
+
+    rng = np.random.default_rng(3)
+    for statuses in ((0, 1, 2), (0, 2), (1,)):
+        n = 500
+        st = rng.choice(statuses, n).astype(np.int8)
+        u = rng.uniform(0, 1200, n).astype(np.float32)
+        res = dict(u_right=u, depth=rng.uniform(1, 50, n).astype(np.float32), status=st)
+        kps = np.zeros(n, dtype=[("x", np.float32)])
+        kps["x"] = rng.uniform(0, 1240, n).astype(np.float32)
+        for mbf in (386.1448, np.float64(386.1448)):
+            a, b = Fr(), Fr()
+            a.mvuRight, _ = to_reference_lists(res, kps, mbf)
+            b.mvuRight = a.mvuRight
+            Mt.prime_u_right(a, res, kps["x"])
+            got, got_d = Mt._u_right(a, with_kinds=True)
+            exp, exp_d = Mt._u_right(b, with_kinds=True)
+            assert got.tobytes() == exp.tobytes() and got_d == exp_d
