@@ -349,6 +349,10 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
 /* orbfe_debug_octree_profile: re-runs the last batch's octree stage with wall-clock marks (100 MHz ticks,
  * 64 per (image, level), 0 = not reached) written by each workgroup's first thread; development aid. */
 int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n);
+/* orbfe_debug_cascade_profile: re-runs the last batch's one-launch pyramid (k_resize_cascade; batches below 32
+ * images) with wall-clock marks, 32 per (image, strip) (0 start, 1 level-0 rows staged, 2 + l level l begins,
+ * 12 + l level l done); *n_strips = the strip count; development aid. */
+int orbfe_debug_cascade_profile(orbfe_handle h, int64_t* marks, int64_t n_marks, int32_t* n_strips);
 /* orbfe_debug_detect_stats: re-runs the last batch's FAST cell stage (idempotent) with counters:
  * stats[0] = cells processed, stats[1] = cells whose iniTh / minTh queues met so that the cell took the
  * one-pass path (both thresholds over the minTh queue), stats[2] = cells that fell back to minTh

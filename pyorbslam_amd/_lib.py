@@ -99,6 +99,7 @@ SIGNATURES = {
     "orbfe_debug_candidates": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_selected": [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)],
     "orbfe_debug_octree_profile": [C.c_void_p, C.c_void_p, C.c_int64],
+    "orbfe_debug_cascade_profile": [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p],
     "orbfe_set_lanes": [C.c_void_p, C.c_int32],
     "orbfe_abi_version": [],
     "orbfe_set_graphs": [C.c_void_p, C.c_int32],

@@ -1994,6 +1994,29 @@ int orbfe_debug_detect_stats(orbfe_handle h, int64_t* stats) {
     });
 }
 
+int orbfe_debug_cascade_profile(orbfe_handle h, int64_t* marks, int64_t n_marks, int32_t* n_strips) {
+    return guarded([&] {
+        if (!h || !marks || !n_strips) throw Error(ORBFE_EINVAL, "null argument");
+        if (h->last_images <= 0 || !h->last_in) throw Error(ORBFE_ESTATE, "run a batch first");
+        const Geo& g = h->geo;
+        const int n = h->last_images;
+        int S = cascade_strips(*h, n);
+        orbfe_ctx::Cascade* cs = nullptr;
+        while (S > 0 && !(cs = find_cascade(*h, S)) && S <= g.lv[g.nlevels - 1].h) S += 4;
+        if (!cs) throw Error(ORBFE_ESTATE, "the last batch did not take the cascade");
+        const int64_t need = (int64_t)n * cs->S * 32;
+        *n_strips = cs->S;
+        if (n_marks < need) throw Error(ORBFE_ECAPACITY, "buffer too small (32 marks per image and strip)");
+        DevBuf<long long> d;
+        d.ensure(need);
+        HIPCK(hipMemset(d.p, 0, need * sizeof(long long)));
+        HIPCK(launch_resize_cascade(g, h->last_in, h->last_pitch, h->d_ws.p, h->d_xt.p, h->d_yt.p, cs->tab.p, cs->S,
+                                    cs->off_b, cs->off_x, cs->lds, n, h->last_stream, nullptr, d.p));
+        HIPCK(hipStreamSynchronize(h->last_stream));
+        HIPCK(hipMemcpy(marks, d.p, need * sizeof(long long), hipMemcpyDeviceToHost));
+    });
+}
+
 int orbfe_debug_octree_profile(orbfe_handle h, int64_t* marks, int64_t n) {
     return guarded([&] {
         if (!h || !marks) throw Error(ORBFE_EINVAL, "null argument");

@@ -95,7 +95,8 @@ size_t detect_lds_bytes(const Geo& g);
 // owned lo, hi} int16 (host resize_strips); LDS: buffer A at 0, B at off_b, the x selectors at off_x
 hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                                  const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
-                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word = nullptr);
+                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word = nullptr,
+                                 long long* prof = nullptr);
 hipError_t prepare_resize_cascade(int lds_bytes);
 // raise the octree kernels' dynamic-LDS attribute for this geometry (outside any stream capture)
 hipError_t prepare_octree(const Geo& g, int maxcell);

@@ -351,7 +351,11 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
                                                      const ResizeY* __restrict__ yt, int wg, int remw, int wgl,
                                                      int* __restrict__ zero_word) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
-    uint32_t* s_src = (uint32_t*)rs_lds;  // staged source rows
+    // staged source rows; the staging's pointers carry their address spaces (generic ones compile to flat
+    // loads, which the compiler must wait for with vmcnt and lgkmcnt together)
+    typedef __attribute__((address_space(3))) uint32_t lds_w32;
+    typedef __attribute__((address_space(1))) const uint32_t glb_u32;
+    lds_w32* s_src = (lds_w32*)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)rs_lds;
     const LevelGeo& L = g.lv[l];
     const LevelGeo& P = g.lv[l - 1];
     int bx, img;
@@ -366,10 +370,10 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     const int ys_lo = yb[0].sy0, ys_hi = yb[nrow - 1].sy1;
     const uintptr_t a0 = (uintptr_t)(src + (int64_t)ys_lo * sstride);
     const int sh0 = (int)(a0 & 3);
-    const uint32_t* gsrc = (const uint32_t*)(a0 - sh0);
+    glb_u32* gsrc = (glb_u32*)(a0 - sh0);
     const int ndw = ((ys_hi - ys_lo) * sstride + P.w + sh0 + 3) >> 2;
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-    const uint32_t src_lds = (uint32_t)(uintptr_t)(lds_u32*)s_src;
+    const uint32_t src_lds = (uint32_t)(uintptr_t)s_src;
     // this thread's group: x selectors / weights straight from the table (issued with the staging loads)
     // remw = 1: the last wave takes the groups past the wg full 64-group chunks (rem < 64 of them) for all
     // rows of the band: lane j owns group wg * 64 + j % rem and rows j / rem, + 64 / rem, ... (a per-lane
@@ -498,51 +502,74 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
 // from LDS, ping-ponging between two buffers (A: level 0 staging and even levels, B: odd levels).
 // tab: per (strip, level) int16 {computed lo, hi, owned lo, hi}; offB / offX: byte offsets of buffer B and
 // of the per-level x selector table in the dynamic LDS.
-__global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
+#ifndef ORBFE_CASCADE_NT
+#define ORBFE_CASCADE_NT 1024
+#endif
+constexpr int kCasNT = ORBFE_CASCADE_NT;  // threads per strip workgroup
+__global__ __launch_bounds__(kCasNT) void k_resize_cascade(Geo g, const uint8_t* __restrict__ in, int64_t in_pitch,
                                                         uint8_t* __restrict__ ws, const ResizeX* __restrict__ xt,
                                                         const ResizeY* __restrict__ yt, const int16_t* __restrict__ tab,
-                                                        int offB, int offX, int* __restrict__ zero_word) {
+                                                        int offB, int offX, int* __restrict__ zero_word,
+                                                        long long* __restrict__ prof) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
     typedef __attribute__((address_space(3))) uint32_t lds_w32;
     const int strip = blockIdx.x, img = blockIdx.y, t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6), nwv = blockDim.x >> 6;
     if (zero_word && strip == 0 && img == 0 && t == 0) *zero_word = 0;
+    // orbfe_debug_cascade_profile: wall-clock marks of the first thread, 32 per (image, strip): 0 start,
+    // 1 staging issued + stored, 2 + l level l's rows may start (after its first barrier), 12 + l level l done
+    long long* pm = prof ? prof + ((int64_t)img * gridDim.x + strip) * 32 : nullptr;
+    auto mark = [&](int id) {
+        if (pm && t == 0) pm[id] = (long long)wall_clock64();
+    };
+    mark(0);
     const int L = g.nlevels;
     const int16_t* st = tab + (int64_t)strip * L * 4;
     const uint32_t baseA = (uint32_t)(uintptr_t)(lds_u32*)rs_lds;
     const uint32_t baseB = baseA + (uint32_t)offB;
     // per group: v_perm selectors, then (a0, a1) weights; its first source column — double-buffered by level
-    // parity: level l + 1's entries are loaded into registers while level l computes
-    uint4* s_xa2[2] = {(uint4*)(rs_lds + offX), (uint4*)(rs_lds + offX) + 2 * g.rs_ngrp};
-    int* s_sx2[2] = {(int*)(s_xa2[1] + 2 * g.rs_ngrp), (int*)(s_xa2[1] + 2 * g.rs_ngrp) + g.rs_ngrp};
-    constexpr int kPre = 2;  // groups per thread held in registers (512 threads: levels up to 4 096 px)
+    // parity: level l + 1's entries are loaded into registers while level l computes.  Every LDS and global
+    // access goes through an address-space-qualified pointer: a generic one (an array of LDS pointers indexed
+    // by the level's parity) compiles to flat loads, which count in vmcnt too — the item loop then waited for
+    // the previous item's global stores before each table read.
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4u lds_u4;
+    typedef __attribute__((address_space(3))) int lds_i32;
+    typedef __attribute__((address_space(1))) const v4u glb_u4;
+    auto u4 = [](v4u v) { return uint4{v.x, v.y, v.z, v.w}; };
+    typedef __attribute__((address_space(1))) const uint32_t glb_u32;
+    auto s_xa_of = [&](int par) { return (lds_u4*)(uintptr_t)(baseA + (uint32_t)offX + (uint32_t)(par * 32 * g.rs_ngrp)); };
+    auto s_sx_of = [&](int par) {
+        return (lds_i32*)(uintptr_t)(baseA + (uint32_t)offX + (uint32_t)(64 * g.rs_ngrp + par * 4 * g.rs_ngrp));
+    };
+    constexpr int kPre = 1024 / kCasNT;  // groups per thread held in registers (levels up to 4 096 px)
     uint4 pq0[kPre], pq1[kPre];
     auto prefetch = [&](int l) {
         if (l >= g.nlevels) return;
-        const uint4* xg = (const uint4*)(xt + g.lv[l].xtab_off);
+        glb_u4* xg = (glb_u4*)(xt + g.lv[l].xtab_off);
         const int ng = (g.lv[l].w + 3) >> 2;
 #pragma unroll
         for (int k = 0; k < kPre; ++k) {
-            const int gi = t + 512 * k;
+            const int gi = t + kCasNT * k;
             if (gi < ng) {
-                pq0[k] = xg[2 * gi];
-                pq1[k] = xg[2 * gi + 1];
+                pq0[k] = u4(xg[2 * gi]);
+                pq1[k] = u4(xg[2 * gi + 1]);
             }
         }
     };
     auto commit = [&](int l) {
-        uint4* sxa = s_xa2[l & 1];
-        int* ssx = s_sx2[l & 1];
+        lds_u4* sxa = s_xa_of(l & 1);
+        lds_i32* ssx = s_sx_of(l & 1);
         const int ng = (g.lv[l].w + 3) >> 2;
 #pragma unroll
         for (int k = 0; k < kPre; ++k) {
-            const int gi = t + 512 * k;
+            const int gi = t + kCasNT * k;
             if (gi < ng) {
                 const uint4 q0 = pq0[k], q1 = pq1[k];
                 auto sel = [&](uint32_t sx) { const uint32_t r = sx - q0.x; return r | ((r + 1) << 16) | 0x0c000c00u; };
-                sxa[2 * gi] = uint4{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
-                sxa[2 * gi + 1] = uint4{q0.y, q0.w, q1.y, q1.w};
+                sxa[2 * gi] = v4u{sel(q0.x), sel(q0.z), sel(q1.x), sel(q1.z)};
+                sxa[2 * gi + 1] = v4u{q0.y, q0.w, q1.y, q1.w};
                 ssx[gi] = (int)(q0.x | ((q1.z - q0.x) << 24));  // sx0, and the 4th pixel's offset (wide levels)
             }
         }
@@ -558,25 +585,26 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
         const int ys_lo = yb[c0].sy0, ys_hi = yb[c1 - 1].sy1;
         const uintptr_t a0 = (uintptr_t)(in + (int64_t)img * in_pitch + (int64_t)ys_lo * g.W);
         src_sh = (uint32_t)(a0 & 3);
-        const uint32_t* gsrc = (const uint32_t*)(a0 - src_sh);
+        glb_u32* gsrc = (glb_u32*)(a0 - src_sh);
         const int ndw = ((ys_hi - ys_lo) * g.W + g.W + (int)src_sh + 3) >> 2;
-        uint32_t* s_src = (uint32_t*)rs_lds;
-        for (int base = 0; base < ndw; base += 512 * kRsSlots / 2) {
+        lds_w32* s_src = (lds_w32*)(uintptr_t)baseA;
+        for (int base = 0; base < ndw; base += kCasNT * kRsSlots / 2) {
             uint32_t v[kRsSlots / 2];
 #pragma unroll
             for (int k = 0; k < kRsSlots / 2; ++k) {
-                const int i = base + t + 512 * k;
+                const int i = base + t + kCasNT * k;
                 v[k] = i < ndw ? gsrc[i] : 0u;
             }
 #pragma unroll
             for (int k = 0; k < kRsSlots / 2; ++k) {
-                const int i = base + t + 512 * k;
+                const int i = base + t + kCasNT * k;
                 if (i < ndw) s_src[i] = v[k];
             }
         }
         src_row0 = ys_lo;
         src_stride = g.W;
     }
+    mark(1);
     for (int l = 1; l < L; ++l) {
         const LevelGeo& Lv = g.lv[l];
         const int c0 = st[4 * l], c1 = st[4 * l + 1], o0 = st[4 * l + 2], o1 = st[4 * l + 3];
@@ -584,65 +612,71 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
         // x selectors / weights of the level (k_resize's per-group form), loaded during the previous level
         commit(l);
         prefetch(l + 1);
-        const uint4* s_xa = s_xa2[l & 1];
-        const int* s_sx0 = s_sx2[l & 1];
+        const lds_u4* s_xa = s_xa_of(l & 1);
+        const lds_i32* s_sx0 = s_sx_of(l & 1);
+        const ResizeY* yb = yt + Lv.ytab_off;
         const uint32_t dst_base = (l & 1) ? baseB : baseA;
         __syncthreads();  // selectors staged; the source rows complete (previous level / staging)
-        const ResizeY* yb = yt + Lv.ytab_off;
+        mark(2 + l);
         uint8_t* gdst = ws + (int64_t)img * g.ws_bytes + Lv.ws_off;
         const int pitch = Lv.pitch;
+        // the level's fields in registers (read from the kernel arguments once, not per item)
+        const int lv_wide = __builtin_amdgcn_readfirstlane(Lv.wide), lv_xvec = __builtin_amdgcn_readfirstlane(Lv.xvec),
+                  lv_area = __builtin_amdgcn_readfirstlane(Lv.area);
         // items (row, chunk), row-major; wave wv takes items wv, wv + nwv, ...: row / chunk advanced
-        // incrementally (uniform), no division per item
-        const int nitems = (c1 - c0) * nch;
-        int r = c0 + wv / nch, ch = wv - (wv / nch) * nch;
-        const int step_r = nwv / nch, step_c = nwv - step_r * nch;
-        for (int item = wv; item < nitems; item += nwv) {
-            const int grp = ch * 64 + lane;
-            if (grp < ngrp) {
-                const uint4 e = s_xa[2 * grp], aa = s_xa[2 * grp + 1];
-                const int sxp = s_sx0[grp];
-                const int sx0 = sxp & 0xFFFFFF;
-                const uint32_t d3 = (uint32_t)sxp >> 24;
-                const ResizeY y = yb[r];
-                const uint32_t lsrc = src_base + src_sh + (uint32_t)sx0;
-                const uint32_t r0 = (uint32_t)((y.sy0 - src_row0) * src_stride), r1 = (uint32_t)((y.sy1 - src_row0) * src_stride);
-                const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
-                auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
-                    const uint32_t A = lsrc + roff, o = A & 3u;
-                    lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
-                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-                    const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
-                    h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
-                                                  __builtin_bit_cast(us2, aa.x), 0u, false);
-                    h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
-                                                  __builtin_bit_cast(us2, aa.y), 0u, false);
-                    h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
-                                                  __builtin_bit_cast(us2, aa.z), 0u, false);
-                    h[3] = Lv.wide ? resize_tap3(A + d3, aa.w)
-                                   : __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
-                                                            __builtin_bit_cast(us2, aa.w), 0u, false);
-                };
-                uint32_t h0[4], h1[4];
-                taps(r0, h0);
-                taps(r1, h1);
-                const int dx = 4 * grp;
-                uint32_t v[4];
+        // incrementally (uniform), no division per item.  (Measured slower here: k_resize_rows' row sets — a
+        // wave walks consecutive rows of one chunk, reusing the previous row's taps — 39 -> 43 us at 8 pairs,
+        // and two items per step with both items' reads issued before either waits, 39 -> 49 us.)
+        // items = rows: wave wv takes rows c0 + wv, + nwv, ...; per row its y entry and offsets once (scalar),
+        // then every 64-group chunk of the row (a uniform loop).  Measured (tools/cascade_profile.py, traces
+        // at 8 pairs): (row, chunk) items 39.7 us, rows 36.4; also tried and slower: row sets with the previous
+        // row's taps reused (43), two items per step with all reads issued first (49), the y entries staged in
+        // LDS instead of scalar loads (42).
+        for (int r = c0 + wv; r < c1; r += nwv) {
+            const ResizeY y = yb[r];
+            const uint32_t r0 = (uint32_t)((y.sy0 - src_row0) * src_stride), r1 = (uint32_t)((y.sy1 - src_row0) * src_stride);
+            const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
+            const bool own = r >= o0 && r < o1;
+            const uint32_t lrow = dst_base + (uint32_t)((r - c0) * pitch);
+            uint8_t* grow = gdst + (int64_t)r * pitch;
+            for (int ch = 0; ch < nch; ++ch) {
+                const int grp = ch * 64 + lane;
+                if (grp < ngrp) {
+                    const uint4 e = u4(s_xa[2 * grp]), aa = u4(s_xa[2 * grp + 1]);
+                    const int sxp = s_sx0[grp];
+                    const uint32_t d3 = (uint32_t)sxp >> 24;
+                    const uint32_t lsrc = src_base + src_sh + (uint32_t)(sxp & 0xFFFFFF);
+                    auto taps = [&](uint32_t roff, uint32_t (&h)[4]) {
+                        const uint32_t A = lsrc + roff, o = A & 3u;
+                        lds_u32* w = (lds_u32*)(uintptr_t)(A - o);
+                        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                        const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, o), d1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+                        h[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.x)),
+                                                      __builtin_bit_cast(us2, aa.x), 0u, false);
+                        h[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.y)),
+                                                      __builtin_bit_cast(us2, aa.y), 0u, false);
+                        h[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.z)),
+                                                      __builtin_bit_cast(us2, aa.z), 0u, false);
+                        h[3] = lv_wide ? resize_tap3(A + d3, aa.w)
+                                       : __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
+                                                                __builtin_bit_cast(us2, aa.w), 0u, false);
+                    };
+                    uint32_t h0[4], h1[4];
+                    taps(r0, h0);
+                    taps(r1, h1);
+                    const int dx = 4 * grp;
+                    uint32_t v[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
-                if (dx + 3 >= Lv.xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
+                    for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
+                    if (dx + 3 >= lv_xvec) {  // FixedPtCast<int, uchar, 22> past the last SIMD block
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (dx + k >= Lv.xvec) v[k] = resize_tail(h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12), Lv.area);
+                        for (int k = 0; k < 4; ++k)
+                            if (dx + k >= lv_xvec) v[k] = resize_tail(h0[k] * (B0 >> 12) + h1[k] * (B1 >> 12), lv_area);
+                    }
+                    const uint32_t px = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+                    *(lds_w32*)(uintptr_t)(lrow + (uint32_t)dx) = px;
+                    if (own) *(uint32_t*)(grow + dx) = px;  // pitch padding past w
                 }
-                const uint32_t px = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-                *(lds_w32*)(uintptr_t)(dst_base + (uint32_t)((r - c0) * pitch + dx)) = px;
-                if (r >= o0 && r < o1) *(uint32_t*)(gdst + (int64_t)r * pitch + dx) = px;  // pitch padding past w
-            }
-            r += step_r;
-            ch += step_c;
-            if (ch >= nch) {
-                ch -= nch;
-                ++r;
             }
         }
         src_base = dst_base;
@@ -650,6 +684,7 @@ __global__ __launch_bounds__(512) void k_resize_cascade(Geo g, const uint8_t* __
         src_row0 = c0;
         src_stride = pitch;
         __syncthreads();  // this level's rows complete before the next level reads them / the selectors change
+        mark(12 + l);
     }
 }
 
@@ -763,6 +798,10 @@ __device__ __forceinline__ int fd_minus_bit(int o, uint64_t m) {
 // cells per k_detect wavefront: 4 (the next cell's ROI loads overlap this one), or 1 for batches too small to
 // give the chip >= 8 waves per CU that way (a frame pair: 610 waves of 4 cells, 2 440 of one)
 constexpr int kFdCells = 4;
+#ifndef ORBFE_FD_SMALL_CELLS
+#define ORBFE_FD_SMALL_CELLS 1
+#endif
+constexpr int kFdSmallCells = ORBFE_FD_SMALL_CELLS;  // cells per wave for small batches (1 or 2)
 
 __device__ __forceinline__ int lanes_below(uint64_t b) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
@@ -3810,8 +3849,9 @@ int detect_cpw(const Geo& g, int n_images, int variant) {
     if (variant == 4) return 4;
     if (variant == 5) return 1;
     // 8 pairs: 39 us with one cell per wave against 47 with four (tools/microbench.py, round 4)
-    return n_images < kSmallBatchImages || (int64_t)n_images * ((g.ncells + kFdCells - 1) / kFdCells) < 8 * 256 ? 1
-                                                                                                                : kFdCells;
+    return n_images < kSmallBatchImages || (int64_t)n_images * ((g.ncells + kFdCells - 1) / kFdCells) < 8 * 256
+               ? kFdSmallCells
+               : kFdCells;
 }
 
 template <int RP, int NS>
@@ -3824,11 +3864,12 @@ static void launch_detect_rp(const Geo& g, const CellGeo* cells, const uint8_t* 
     // time depends on occupancy; 1 / 2 / 3: the ablations (tools/microbench.py)
     const size_t lds = detect_lds_bytes(g) + (variant == 8 ? 6144 : variant == 9 ? 12288 : 0);
     auto k = variant == 1 ? k_detect<1, RP, NS, kFdCells> : variant == 2 ? k_detect<2, RP, NS, kFdCells>
-           : variant == 3 ? k_detect<3, RP, NS, kFdCells> : cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>;
+           : variant == 3 ? k_detect<3, RP, NS, kFdCells> : cpw == 1 ? k_detect<0, RP, NS, 1>
+           : cpw == kFdSmallCells ? k_detect<0, RP, NS, kFdSmallCells> : k_detect<0, RP, NS, kFdCells>;
 #else
     const size_t lds = detect_lds_bytes(g);
-    auto k = stats ? (cpw == 1 ? k_detect<0, RP, NS, 1, true> : k_detect<0, RP, NS, kFdCells, true>)  // debug counters
-                   : (cpw == 1 ? k_detect<0, RP, NS, 1> : k_detect<0, RP, NS, kFdCells>);
+    auto k = stats ? (cpw == kFdSmallCells ? k_detect<0, RP, NS, kFdSmallCells, true> : k_detect<0, RP, NS, kFdCells, true>)  // debug counters
+                   : (cpw == kFdSmallCells ? k_detect<0, RP, NS, kFdSmallCells> : k_detect<0, RP, NS, kFdCells>);
 #endif
     hipLaunchKernelGGL(k, grid, blk, lds, s, g, cells, in, in_pitch, ws, cell_count, slots, stats);
 }
@@ -3930,11 +3971,11 @@ hipError_t prepare_octree(const Geo& g, int maxcell) {
 
 hipError_t launch_resize_cascade(const Geo& g, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                                  const ResizeY* yt, const int16_t* strips, int n_strips, int off_b, int off_x,
-                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word) {
+                                 int lds_bytes, int n_images, hipStream_t s, int* zero_word, long long* prof) {
     if (g.nlevels < 2 || n_images <= 0) return hipSuccess;
     if (lds_bytes > lds_limit((const void*)k_resize_cascade)) return hipErrorInvalidConfiguration;  // prepare_resize_cascade was not run
-    hipLaunchKernelGGL(k_resize_cascade, dim3(n_strips, n_images), dim3(512), (size_t)lds_bytes, s, g, in, in_pitch, ws,
-                       xt, yt, strips, off_b, off_x, zero_word);
+    hipLaunchKernelGGL(k_resize_cascade, dim3(n_strips, n_images), dim3(kCasNT), (size_t)lds_bytes, s, g, in, in_pitch, ws,
+                       xt, yt, strips, off_b, off_x, zero_word, prof);
     return hipGetLastError();
 }
 
@@ -3981,6 +4022,10 @@ static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, con
 // k_orb can carry the stereo buckets when the (H + 1) counters fit its s_h buffer (256-thread workgroups)
 bool orb_fuses_bucket(const Geo& g) { return g.H + 1 <= 4 * kHPairs * kHDw; }
 
+#ifndef ORBFE_ORB_SMALL_KPW
+#define ORBFE_ORB_SMALL_KPW 2
+#endif
+constexpr int kOrbSmallKpw = ORBFE_ORB_SMALL_KPW;  // keypoints per wave below the 4-keypoint threshold (2 or 4)
 // keypoints per wave for a batch: 8 (4 waves per workgroup: 953 -> 914 us per 256 pairs against 4, same-box
 // A/B, round 1) while the batch gives >= 16 waves per CU that way, else 4, else 2 (a frame pair: 508 waves of
 // 8 keypoints, 2 028 of 2).  Variants (microbench): 1 / 9 / 2 force 8 / 4 / 2.
@@ -3990,7 +4035,7 @@ int orb_kpw(const Geo& g, int n_images, int variant) {
     if (variant == 2 || variant == 12) return 2;
     for (int k : {8, 4})
         if ((int64_t)orb_waves(g, k) * n_images >= 16 * 256) return k;
-    return 2;
+    return kOrbSmallKpw;
 }
 
 hipError_t launch_orb(const Geo& g, const uint8_t* in, int64_t in_pitch, const uint8_t* ws, const uint32_t* lvl_kp,
