@@ -2080,10 +2080,10 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         constexpr int EB = (2048 + 1 + NT - 1) / NT;  // bins (+ the total) per thread
         constexpr int EP = (2816 + NT - 1) / NT;      // closed-form enumeration: sum over depths <= D0 of nodes
         constexpr int NW = NT / 64;
-        __shared__ int s_red[NW];
+        __shared__ int s_red[2][NW];
+        int red_par = 0;
         __shared__ int s_dc[3][16];                    // per depth: listed nodes, of which single-key, >= 2 keys
-        __shared__ int s_cw[NW][16];                   // radix: per-wave digit counts
-        __shared__ int s_co[NW][16];                   // radix: per-wave digit offsets
+        __shared__ int s_cw[2][NW][16];                // radix: per-wave digit counts (by pass parity)
         __shared__ int s_m[4];
         const int lane = t & 63, wv = t >> 6;
         const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -2098,26 +2098,41 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                 s0 += x;
             }
             const int inc = wave_incl_scan_dpp(s0);
-            if (lane == 63) s_red[wv] = inc;
+            // the wave totals alternate between two buffers: the next scan writes the other one, and the one
+            // after it comes after the next scan's barrier, i.e. after every wave has read this one
+            int* red = s_red[red_par];
+            red_par ^= 1;
+            if (lane == 63) red[wv] = inc;
             __syncthreads();
             int off = 0, tot = 0;
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
-                const int r = s_red[i];
+                const int r = red[i];
                 off += i < wv ? r : 0;
                 tot += r;
             }
             const int ex = off + inc - s0;
 #pragma unroll
             for (int k = 0; k < E; ++k) v[k] += ex;
-            __syncthreads();
             return tot;
+        };
+        // workgroup OR of a predicate, one barrier (the scans' alternating wave-total buffers)
+        auto bor = [&](bool q) -> bool {
+            int* red = s_red[red_par];
+            red_par ^= 1;
+            const bool wq = __ballot(q) != 0ull;
+            if (lane == 0) red[wv] = wq;
+            __syncthreads();
+            int any = 0;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) any |= red[i];
+            return any != 0;
         };
         auto pack = [](uint32_t code, int n, int dp) {
             return (uint64_t)code | ((uint64_t)(((uint32_t)n << 8) | (uint32_t)dp) << 32);
         };
         for (int i = t; i < NC; i += NT) d.proc[i] = 0;  // (ordered before use by bscan's barriers)
-        if (t < 16 * NW) (&s_cw[0][0])[t] = 0;
+        for (int i = t; i < 2 * 16 * NW; i += NT) (&s_cw[0][0][0])[i] = 0;
         // cumulative bin counts, bins[B] = K
         {
             int v[EB];
@@ -2254,8 +2269,12 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         // children counts of the nodes deeper than D0 among the division candidates sel(p): one sweep of every
         // thread over the cached keys
         auto deep_counts = [&](auto&& sel) {
+            // (a pass without deep candidates costs one barrier: the OR)
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < LP; ++k) any |= sel(t * LP + k) && node_dep(cur, t * LP + k) >= D0;
             if (t == 0) s_m[0] = 0;
-            __syncthreads();
+            if (!bor(any)) return;
 #pragma unroll
             for (int k = 0; k < LP; ++k) {
                 const int p = t * LP + k;
@@ -2268,7 +2287,6 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             }
             __syncthreads();
             const int nd = s_m[0];
-            if (nd == 0) return;
             deep_sort_l(nd, cur);
             __syncthreads();
             for_cached(t, NT, std::integral_constant<int, 1>{}, [&](int kk, uint32_t, uint32_t cd) {
@@ -2293,6 +2311,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             }
         };
         bool ovf = false;
+        int rpass = 0;  // radix passes so far (the digit-count buffer's parity)
         for (int iter = 0; mode >= 2; ++iter) {
             if (iter > 4 * CAPL + 64) {  // cannot happen (each pass grows the list or finishes); never hang
                 if (t == 0) atomicOr(overflow, 2);
@@ -2338,6 +2357,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                 // children, positions < C) by size descending, equal sizes in creation order descending (=
                 // position ascending), divided until the list reaches N
                 auto cand = [&](int p) { return p < C && node_cnt(cur, p) > 1; };
+                if (t == 0) s_m[3] = 0;  // (read last iteration after its proc barrier; the atomics come after 3+ barriers)
                 deep_counts(cand);
                 if (iter == 0) mark(43);
                 // candidates in position order -> (size, position | children << 16) at their compacted index
@@ -2398,29 +2418,33 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                             for (int bit = 0; bit < 4; ++bit) m &= ((dg[k] >> bit) & 1) ? bb[j][bit] : ~bb[j][bit];
                             rk[k] += __popcll(m & lt) + (j < k && dg[j] == dg[k]);
                         }
-                        atomicAdd(&s_cw[wv][dg[k]], 1);
+                        atomicAdd(&s_cw[rpass & 1][wv][dg[k]], 1);
                     }
+                    // the other buffer, for the next pass: its readers (the previous pass) are past that pass's
+                    // last barrier; the next pass's counts come after this pass's two
+                    for (int i = t; i < 16 * NW; i += NT) (&s_cw[(rpass + 1) & 1][0][0])[i] = 0;
                     __syncthreads();
-                    if (t < 64) {  // offset of (wave w, digit b): every smaller digit, then earlier waves
-                        int tot = 0;
-                        if (t < 16)
-                            for (int w = 0; w < NW; ++w) {
-                                s_co[w][t] = tot;
-                                tot += s_cw[w][t];
-                                s_cw[w][t] = 0;  // for the next pass (its counts come after two barriers)
-                            }
-                        const int base = wave_incl_scan_dpp(tot) - tot;  // digits below t (lanes >= 16: 0)
-                        if (t < 16)
-                            for (int w = 0; w < NW; ++w) s_co[w][t] += base;
-                    }
-                    __syncthreads();
+                    // every wave its own offsets, lane b = digit b: every smaller digit, then earlier waves' b
+                    int below = 0, tot = 0;
+                    if (lane < 16) {
 #pragma unroll
-                    for (int k = 0; k < LP; ++k)
+                        for (int w = 0; w < NW; ++w) {
+                            const int c = s_cw[rpass & 1][w][lane];
+                            below += w < wv ? c : 0;
+                            tot += c;
+                        }
+                    }
+                    const int myoff = wave_incl_scan_dpp(tot) - tot + below;  // (lanes >= 16 add nothing)
+                    ++rpass;
+#pragma unroll
+                    for (int k = 0; k < LP; ++k) {
+                        const int o = __shfl(myoff, dg[k] < 0 ? 0 : dg[k]) + rk[k];
                         if (dg[k] >= 0) {
-                            const int e = t * LP + k, o = s_co[wv][dg[k]] + rk[k];
+                            const int e = t * LP + k;
                             kb[o] = ka[e];
                             pb[o] = pa[e];
                         }
+                    }
                     __syncthreads();
                     int* tk = ka; ka = kb; kb = tk;
                     int* tp = pa; pa = pb; pb = tp;
@@ -2436,8 +2460,6 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                     gv[k] = e < M ? (nc - 1) | (nc << 16) : 0;
                 }
                 bscan(gv);
-                if (t == 0) s_m[3] = 0;
-                __syncthreads();
 #pragma unroll
                 for (int k = 0; k < LP; ++k) {
                     const int e = t * LP + k;
@@ -2470,7 +2492,8 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
                         if (p < S && !d.proc[p]) nxt[Cn + kp[k]] = cur[p];
                     }
                 }
-                __syncthreads();
+                // proc[p] is read only by p's own thread (above and in kp): it clears it; the loop's last barrier
+                // orders that before the next iteration's marks
 #pragma unroll
                 for (int k = 0; k < LP; ++k)
                     if (t * LP + k < S) d.proc[t * LP + k] = 0;
@@ -3952,9 +3975,13 @@ static int lds_limit(const void* fn) {
 
 hipError_t prepare_resize_cascade(int lds_bytes) { return raise_lds((const void*)k_resize_cascade, lds_bytes); }
 
+#ifndef ORBFE_OB_SMALL_NT
+#define ORBFE_OB_SMALL_NT 1024
+#endif
+constexpr int kObSmallNT = ORBFE_OB_SMALL_NT;  // k_octree_bins threads for small batches
 static const void* octree_bins_fn(const Geo& g, bool wide) {
     const bool reg = octree_reg_passes(g.max_ncap);
-    return wide ? (reg ? (const void*)k_octree_bins<1024, true> : (const void*)k_octree_bins<1024, false>)
+    return wide ? (reg ? (const void*)k_octree_bins<kObSmallNT, true> : (const void*)k_octree_bins<kObSmallNT, false>)
                 : (reg ? (const void*)k_octree_bins<kObThreads, true> : (const void*)k_octree_bins<kObThreads, false>);
 }
 
@@ -3989,9 +4016,9 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
         const void* fn = octree_bins_fn(g, wide);
         if ((int)lds > lds_limit(fn)) return hipErrorInvalidConfiguration;  // prepare_octree
         const bool reg = octree_reg_passes(g.max_ncap);
-        auto k = wide ? (reg ? k_octree_bins<1024, true> : k_octree_bins<1024, false>)
+        auto k = wide ? (reg ? k_octree_bins<kObSmallNT, true> : k_octree_bins<kObSmallNT, false>)
                       : (reg ? k_octree_bins<kObThreads, true> : k_octree_bins<kObThreads, false>);
-        hipLaunchKernelGGL(k, dim3(n_images, g.nlevels), dim3(wide ? 1024 : kObThreads), lds, s, g, cells, cell_count,
+        hipLaunchKernelGGL(k, dim3(n_images, g.nlevels), dim3(wide ? kObSmallNT : kObThreads), lds, s, g, cells, cell_count,
                            slots, octab, lvl_kp, lvl_count, overflow, maxcell, kd, prof);
         return hipGetLastError();
     }
