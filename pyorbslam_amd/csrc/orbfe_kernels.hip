@@ -1834,8 +1834,8 @@ __host__ __device__ inline size_t ob_carve(int NC, int B, int CM, int TW, int KB
     return o;
 }
 
-// NT threads: 256 (large batches: the workgroups of many images share the CUs) or 1 024 for small batches,
-// where one image's level-0 workgroup is the critical path and its key sweeps take 4x fewer rounds.
+// NT threads: 256 (large batches: the workgroups of many images share the CUs) or kObSmallNT (512) for small batches,
+// where a few images' workgroups are the critical path.
 template <int NT, bool FLAT>
 __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __restrict__ cells,
                                                             const int* __restrict__ cell_count,
@@ -3976,9 +3976,12 @@ static int lds_limit(const void* fn) {
 hipError_t prepare_resize_cascade(int lds_bytes) { return raise_lds((const void*)k_resize_cascade, lds_bytes); }
 
 #ifndef ORBFE_OB_SMALL_NT
-#define ORBFE_OB_SMALL_NT 1024
+#define ORBFE_OB_SMALL_NT 512
 #endif
-constexpr int kObSmallNT = ORBFE_OB_SMALL_NT;  // k_octree_bins threads for small batches
+// k_octree_bins threads for small batches: 512 (8 pairs: 35.5 -> 33.1 us against 1 024 — the passes run on
+// <= 512 list positions, so waves 8-15 only added issue contention; level 0's key sweep is slower, but the
+// kernel's critical path is a small level's careful iterations; tools/octree_profile.py, round 5)
+constexpr int kObSmallNT = ORBFE_OB_SMALL_NT;
 static const void* octree_bins_fn(const Geo& g, bool wide) {
     const bool reg = octree_reg_passes(g.max_ncap);
     return wide ? (reg ? (const void*)k_octree_bins<kObSmallNT, true> : (const void*)k_octree_bins<kObSmallNT, false>)
@@ -4011,7 +4014,7 @@ hipError_t launch_octree(const Geo& g, const CellGeo* cells, const int* cell_cou
                          int maxcell, int n_images, hipStream_t s, int variant, long long* prof) {
     if (g.oct_v == 0) {
         const size_t lds = octree_bins_lds_bytes(g, maxcell);
-        // 1 024 threads for small batches (variant 1 / 2 force 256 / 1 024, tools/microbench.py)
+        // kObSmallNT threads for small batches (variant 1 / 2 force 256 / kObSmallNT, tools/microbench.py)
         const bool wide = variant == 2 || (variant != 1 && n_images < kSmallBatchImages);
         const void* fn = octree_bins_fn(g, wide);
         if ((int)lds > lds_limit(fn)) return hipErrorInvalidConfiguration;  // prepare_octree
