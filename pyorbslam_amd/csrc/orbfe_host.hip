@@ -125,7 +125,7 @@ struct orbfe_ctx {
     hipEvent_t lane_done[kLanes] = {};
     hipEvent_t lane_fork = nullptr;
     hipStream_t last_stream = nullptr;
-    hipEvent_t batch_done = nullptr;   // recorded on last_stream at the end of every batch enqueue
+    hipEvent_t batch_done = nullptr;   // recorded on last_stream when another stream needs the last batch
     bool batch_done_rec = false;
     const uint8_t* last_in = nullptr;  // device input of the last extraction
     int64_t last_pitch = 0;
@@ -886,10 +886,21 @@ void stereo_range(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int p0, int 
 
 // Marks the end of a batch enqueue on s: orbfe_batch_pack_device orders its k_pack after it, whatever
 // stream the caller packs on.
+// A batch enqueue only notes that its results are pending on last_stream; the event is recorded when a call
+// on another stream needs them (wait_batch_done).  Recording it at every enqueue put a marker packet between a
+// handle's consecutive chains: with two handles on two queues it delayed the next chain's first kernel by
+// ~6 us (8-pair step 0.162 -> 0.159 ms with one handle, tools/small_batch.py).
 void record_batch_done(orbfe_ctx& c, hipStream_t s) {
-    if (!c.batch_done) HIPCK(hipEventCreateWithFlags(&c.batch_done, hipEventDisableTiming));
-    HIPCK(hipEventRecord(c.batch_done, s));
+    (void)s;
     c.batch_done_rec = true;
+}
+
+// order `caller` after the handle's last batch (a no-op on the batch's own stream)
+void wait_batch_done(orbfe_ctx& c, hipStream_t caller) {
+    if (!c.batch_done_rec || caller == c.last_stream) return;
+    if (!c.batch_done) HIPCK(hipEventCreateWithFlags(&c.batch_done, hipEventDisableTiming));
+    HIPCK(hipEventRecord(c.batch_done, c.last_stream));
+    HIPCK(hipStreamWaitEvent(caller, c.batch_done, 0));
 }
 
 void enqueue_stereo_batch(orbfe_ctx& c, int n_pairs, double bf, float fx, hipStream_t s) {
@@ -1495,7 +1506,7 @@ int orbfe_batch_pack_device(orbfe_handle h, uint8_t* d_records, int64_t rec_byte
         PackArgs a{h->d_count.p, h->d_kps.p, h->d_desc.p, h->d_uR.p, h->d_depth.p, h->d_status.p, h->geo.kp_cap,
                    rec_bytes};
         // the records are read after the batch that produced them, on whichever stream the caller packs
-        if (h->batch_done_rec) HIPCK(hipStreamWaitEvent((hipStream_t)hip_stream, h->batch_done, 0));
+        wait_batch_done(*h, (hipStream_t)hip_stream);
         HIPCK(launch_pack(a, d_records, pair0, n_pairs, (hipStream_t)hip_stream));
     });
 }
@@ -1531,7 +1542,7 @@ int orbfe_batch_pack_compact_device(orbfe_handle h, uint8_t* d_records, int64_t 
                    rec_bytes};
         CompactScales sc{};
         for (int l = 0; l < kMaxLevels; ++l) sc.inv_scale[l] = l < h->geo.nlevels ? h->geo.inv_scale[l] : 1.f;
-        if (h->batch_done_rec) HIPCK(hipStreamWaitEvent((hipStream_t)hip_stream, h->batch_done, 0));
+        wait_batch_done(*h, (hipStream_t)hip_stream);
         HIPCK(launch_pack_compact(a, sc, d_records, pair0, n_pairs, (hipStream_t)hip_stream));
     });
 }
