@@ -62,9 +62,10 @@ VALU_PEAK_FAST_CLASS_GIPS = 256 * 4 * 2.4 / 2.4
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16 spec, per direction
 STAGES = ["resize", "detect", "octree", "describe", "stereo"]  # orbfe_profile_read order (ORBFE_NSTAGES)
-STAGE_KERNELS = {"resize": "k_resize_rows (x7 levels)", "detect": "k_detect", "octree": "k_octree",
-                 "describe": "k_orb (IC angle + per-keypoint 7x7 blur + steered BRIEF)",
-                 "stereo": "k_stereo_bucket + k_stereo"}
+STAGE_KERNELS = {"resize": "k_resize_rows (x7 levels)", "detect": "k_detect", "octree": "k_octree_bins",
+                 "describe": "k_orb (IC angle + per-keypoint 7x7 blur + steered BRIEF; its first workgroups build "
+                             "the stereo row buckets)",
+                 "stereo": "k_stereo"}
 CAMERAS = {(1241, 376): ("kitti", "KITTI 1241x376"), (752, 480): ("euroc", "EuRoC 752x480")}
 C4_TOTAL_PAIRS = 64    # BASELINE.json configs[3]
 

@@ -12,7 +12,7 @@ import sys
 from pathlib import Path
 
 STAGES = {"resize": ["k_resize_rows", "k_resize"], "detect": ["k_detect"], "octree": ["k_octree_bins", "k_octree"],
-          "describe": ["k_orb"], "stereo": ["k_stereo_bucket", "k_stereo"]}
+          "describe": ["k_orb"], "stereo": ["k_stereo", "k_stereo_bucket"]}  # (buckets inside k_orb since round 5)
 
 
 def stamp() -> dict:
