@@ -358,9 +358,10 @@ class Shard:
         import torch
         from pyorbslam_amd.batch import StereoFrontEnd, camera_constants
         self.bf, self.fx = camera or camera_constants(width, height)
-        # at least 4 pairs per handle: a one-rank share of 8-way C4 (8 pairs) runs 0.18 ms per step as 2 handles,
-        # 0.29 as 4 (tools/small_batch.py, round 4): tiny handles only add latency-bound launches
-        S = max(1, min(streams, -(-n_pairs // 4)))
+        # at least 3 pairs per handle: a one-rank share of 8-way C4 (8 pairs) runs 0.136 ms per step as 3 handles,
+        # 0.141 as 2 and, depending on how the 4 streams land on the hardware queues, 0.135-0.30 as 4
+        # (tools/small_batch.py, round 5): tiny handles only add latency-bound launches
+        S = max(1, min(streams, -(-n_pairs // 3)))
         self.counts = [shard(n_pairs, S, i)[1] for i in range(S)]
         self.fes = [StereoFrontEnd(width, height, max_pairs=max(c, 1), nfeatures=nfeatures, lanes=lanes)
                     for c in self.counts]
