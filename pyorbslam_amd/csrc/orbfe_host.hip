@@ -987,7 +987,7 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
                         prof_mark(c, q, 5);
                     });
     } else {
-        HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), s));
+        // the lane streams, events and each chunk's pyramid tables exist before a graph capture starts
         if (!c.lane_stream[0]) {
             for (int k = 0; k < kLanes; ++k) {
                 HIPCK(hipStreamCreateWithFlags(&c.lane_stream[k], hipStreamNonBlocking));
@@ -995,20 +995,37 @@ void enqueue_frontend(orbfe_ctx& c, const uint8_t* d_in, int64_t pitch, int n_pa
             }
             HIPCK(hipEventCreateWithFlags(&c.lane_fork, hipEventDisableTiming));
         }
-        HIPCK(hipEventRecord(c.lane_fork, s));
+        auto chunk = [&](int k, int& p0, int& p1) {
+            p0 = (int)((int64_t)n_pairs * k / K);
+            p1 = (int)((int64_t)n_pairs * (k + 1) / K);
+        };
         for (int k = 0; k < K; ++k) {
-            const int p0 = (int)((int64_t)n_pairs * k / K), p1 = (int)((int64_t)n_pairs * (k + 1) / K);
+            int p0, p1;
+            chunk(k, p0, p1);
             prepare_pyramid(c, 2 * (p1 - p0));
-            hipStream_t ls = c.lane_stream[k];
-            HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
-            const bool fuse = orb_fuses_bucket(c.geo);
-            const StereoArgs sa = stereo_args(c, d_in, pitch, p0, bf, fx);
-            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k, false, fuse ? &sa : nullptr);
-            stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls, fuse);
-            if (k == 0) prof_mark(c, ls, 5);
-            HIPCK(hipEventRecord(c.lane_done[k], ls));
         }
-        for (int k = 0; k < K; ++k) HIPCK(hipStreamWaitEvent(s, c.lane_done[k], 0));
+        // fork / join with events; under ORBFE_GRAPH_BATCH the whole fork / join is captured as ONE graph with
+        // K parallel branches (the lane streams join the capture through the fork event)
+        run_enqueue(c, ORBFE_GRAPH_BATCH,
+                    {2, bits_of(d_in), (uint64_t)pitch, (uint64_t)n_pairs, bits_of(bf), bits_of(fx), (uint64_t)K}, s,
+                    [&](hipStream_t q) {
+                        HIPCK(hipMemsetAsync(c.d_overflow.p, 0, sizeof(int), q));
+                        HIPCK(hipEventRecord(c.lane_fork, q));
+                        for (int k = 0; k < K; ++k) {
+                            int p0, p1;
+                            chunk(k, p0, p1);
+                            hipStream_t ls = c.lane_stream[k];
+                            HIPCK(hipStreamWaitEvent(ls, c.lane_fork, 0));
+                            const bool fuse = orb_fuses_bucket(c.geo);
+                            const StereoArgs sa = stereo_args(c, d_in, pitch, p0, bf, fx);
+                            extract_range(c, d_in, pitch, 2 * p0, 2 * (p1 - p0), ls, k == 0, k, false,
+                                          fuse ? &sa : nullptr);
+                            stereo_range(c, d_in, pitch, p0, p1 - p0, bf, fx, ls, fuse);
+                            if (k == 0) prof_mark(c, ls, 5);
+                            HIPCK(hipEventRecord(c.lane_done[k], ls));
+                        }
+                        for (int k = 0; k < K; ++k) HIPCK(hipStreamWaitEvent(q, c.lane_done[k], 0));
+                    });
     }
     if (c.prof_on && c.prof_n < c.prof_max) ++c.prof_n;
     c.last_in = d_in;

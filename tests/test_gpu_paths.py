@@ -56,6 +56,29 @@ def test_graph_replay_equals_stream_path(n_pairs):
     assert kl.tobytes() == okl.tobytes() and np.array_equal(dl, odl)
 
 
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_multilane_graph_equals_stream_path(lanes):
+    """the multi-lane fork / join (orbfe_set_lanes: the pairs as `lanes` chunks on internal
+    streams, forked from and joined into the caller's stream with events) captured as ONE graph with parallel
+    branches, replayed across two input buffers, against the one-lane stream path."""
+    torch = pytest.importorskip("torch")
+    from pyorbslam_amd.batch import StereoFrontEnd
+    n_pairs = 8
+    bufs = [torch.from_numpy(synth.make_batch(n_pairs, seed0=s0)).cuda() for s0 in (520, 620)]
+    ref = StereoFrontEnd(max_pairs=n_pairs, lanes=1, graphs=False)
+    fe = StereoFrontEnd(max_pairs=n_pairs, lanes=lanes, graphs=True)
+    st = torch.cuda.Stream()
+    for it in range(5):
+        d = bufs[it % 2]
+        ref.enqueue(d, n_pairs)
+        fe.enqueue(d, n_pairs, stream_ptr=st.cuda_stream)
+        torch.cuda.synchronize()
+        _same_batches(ref, fe, n_pairs)
+        assert fe.overflow() == 0
+    gs = fe.graph_stats()
+    assert gs["captures"] == 2 and gs["launches"] == 5 and gs["cached"] == 2, gs
+
+
 def test_graph_cache_eviction_with_new_inputs_every_step():
     """with graphs on and a new input buffer every step, every enqueue captures a graph
     and, past the 8-entry cache, evicts the oldest one while earlier steps are still queued on the caller's

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--handles", default="1,2,4", help="handle counts to try (pairs split by dist.shard)")
     ap.add_argument("--graphs", default="0,1", help="graph settings to try")
     ap.add_argument("--no-frame", action="store_true")
+    ap.add_argument("--lanes", default="1", help="orbfe_set_lanes settings to try (internal fork / join chunks)")
     a = ap.parse_args()
     import os
     from pyorbslam_amd.dist import shard
@@ -31,10 +32,11 @@ def main():
     out = {}
     imgs = torch.from_numpy(synth.make_batch(8, seed0=0)).to(dev)
     out["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
-    for graphs in [bool(int(v)) for v in a.graphs.split(",")]:
-        for handles in [int(v) for v in a.handles.split(",")]:
+    for graphs, handles, lanes in [(bool(int(g)), int(h), int(ln)) for g in a.graphs.split(",")
+                                   for h in a.handles.split(",") for ln in a.lanes.split(",")]:
+        if True:
             parts = [shard(8, handles, i) for i in range(handles)]
-            fes = [StereoFrontEnd(max_pairs=n, lanes=1, graphs=graphs) for _, n in parts]
+            fes = [StereoFrontEnd(max_pairs=n, lanes=lanes, graphs=graphs) for _, n in parts]
             sts = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(handles - 1)]
 
             def step():
@@ -56,7 +58,7 @@ def main():
                 step()
                 torch.cuda.synchronize(dev)
                 lat.append(time.perf_counter() - t)
-            out[f"pairs8_{handles}h_graphs{int(graphs)}"] = {"ms_per_step": round(ms, 4),
+            out[f"pairs8_{handles}h{'' if lanes == 1 else f'_{lanes}lanes'}_graphs{int(graphs)}"] = {"ms_per_step": round(ms, 4),
                                                              "latency_ms_p50": round(1e3 * float(np.median(lat)), 4),
                                                              "pairs_per_s": round(8 / ms * 1e3, 1)}
             del fes
