@@ -745,11 +745,26 @@ std::unique_ptr<orbfe_ctx::Cascade> resize_strips(const orbfe_ctx& c, int S) {
 // (uploads, kernel attributes) before an enqueue is captured: prepare_pyramid runs outside the capture.
 constexpr int kCascadeImages = kSmallBatchImages;
 
+// compute units of the current device (one strip workgroup per CU: a 1 024-thread strip is a latency chain,
+// and two of them on one CU run at half speed each)
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int v = 0;
+        cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    }
+    return cus[dev];
+}
+
+// strips per image: at most one workgroup per CU for the batch (8 images on 256 CUs: 32 strips, not 35 of which
+// 24 CUs would hold two: 33 -> ~20 us), at least 3 top-level rows each, at least 4 strips
 int cascade_strips(const orbfe_ctx& c, int n) {
     if (c.cascade_force) return c.cascade_force;
     if (n >= kCascadeImages || c.geo.nlevels < 2) return -1;
     const int htop = c.geo.lv[c.geo.nlevels - 1].h;
-    return std::max(4, std::min((512 + n - 1) / n, std::max(4, htop / 3)));
+    return std::max(4, std::min(device_cus() / std::max(n, 1), std::max(4, htop / 3)));
 }
 
 orbfe_ctx::Cascade* find_cascade(orbfe_ctx& c, int S) {
