@@ -74,6 +74,13 @@ constexpr int kRsRows = ORBFE_RS_ROWS;  // k_resize output rows per workgroup (b
 constexpr int kSmallBatchImages = 32;
 // k_octree candidates kept in LDS (with the node arrays <= 80 KiB: two workgroups per CU)
 constexpr int kOctKeys = 7424;
+// k_octree_bins: keys per block of the first sweep's key -> cell table (log2); a key walks forward from its
+// block's first cell over the cells the block spans
+#ifndef ORBFE_OB_KBLK_SH
+#define ORBFE_OB_KBLK_SH 4  // 16 keys (64: octree 0.421 -> 0.408 ms standalone, 8 pairs 32.9 -> 31.8 us; 8: LDS, 0.574)
+#endif
+constexpr int kObKblkSh = ORBFE_OB_KBLK_SH;
+constexpr int kObKblkMax = 32768 >> kObKblkSh;  // table entries (keys past them walk from the last one)
 
 struct ResizeX {
     int32_t sx;
@@ -110,7 +117,7 @@ struct Geo {
     int fd_alt;          // k_detect: largest cell slot_cap (minTh survivors staged in the ROI area)
     int oct_bins_max;    // k_octree (bins): most bins of any level
     int oct_tab_max;     // k_octree (bins): most X + Y table words of any level
-    int oct_kblk_max;    // k_octree (bins): most 64-key blocks of any level (key_cap / 64 + 1)
+    int oct_kblk_max;    // k_octree (bins): most key blocks of any level (key_cap >> kObKblkSh + 1)
     int oct_v;           // k_octree implementation: 0 bins (default), 1 the per-candidate pass kernel (automatic
                          // when the bins' LDS would exceed 150 KiB, or orbfe_set_octree_kernel)
     int umax[16];

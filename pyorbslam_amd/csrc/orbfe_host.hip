@@ -509,7 +509,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         octree_tables(Lg, Lg.n_feat, c.octab);
         g.oct_bins_max = std::max(g.oct_bins_max, Lg.oct_bins);
         g.oct_tab_max = std::max(g.oct_tab_max, Lg.oct_nx + Lg.oct_ny);
-        g.oct_kblk_max = std::max(g.oct_kblk_max, std::min(Lg.key_cap / 64 + 1, 512));
+        g.oct_kblk_max = std::max(g.oct_kblk_max, std::min((Lg.key_cap >> kObKblkSh) + 1, kObKblkMax));
         Lg.kp_off = kp_off;
         kp_off += Lg.kp_cap;
         g.max_ncap = std::max(g.max_ncap, Lg.kp_cap);

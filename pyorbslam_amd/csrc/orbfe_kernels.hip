@@ -1753,37 +1753,48 @@ __device__ __forceinline__ int chunk_excl_scan(int (&v)[N]) {
     return __builtin_amdgcn_readlane(inc, 63);
 }
 
-// One key per lane, its bin b (0xFFFFFFFF: no key) and value v = response << 24 | 0xFFFFFF - index.  Lanes
-// of a wave mostly hold consecutive keys of one cell, i.e. a few bins each held by a run of lanes, so the
-// histogram / maximum go through the run heads / tails instead of 64 same-address LDS atomics:
-// counts: the head of each run of equal bins (across the wave) adds the run length; maxima: a segmented
-// max inside each 16-lane row (idempotent, so reaching further than the run is harmless) and the last
-// lane of each run within a row applies it.
-__device__ __forceinline__ void bin_add_runs(uint32_t* hist, uint32_t* bmax, uint32_t b, uint32_t v) {
+// NB rounds of one key per lane (the atomics of all rounds after their scans), its bin b (0xFFFFFFFF: no key)
+// and value v = response << 24 | 0xFFFFFF - index.  Lanes of a wave mostly hold consecutive keys of one
+// cell, i.e. a few bins each held by a run of lanes, so the histogram / maximum go through the run heads /
+// tails instead of 64 same-address LDS atomics: counts: the head of each run of equal bins (across the
+// wave) adds the run length; maxima: a segmented max inside each 16-lane row (idempotent, so reaching
+// further than the run is harmless) and the last lane of each run within a row applies it.
+template <int NB>
+__device__ __forceinline__ void bin_add_runs(uint32_t* hist, uint32_t* bmax, const uint32_t (&bb)[NB],
+                                             const uint32_t (&vv)[NB]) {
     const int lane = threadIdx.x & 63;
-    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
-    const bool valid = b != 0xFFFFFFFFu;
-    const bool head = valid && (lane == 0 || prev != b);
-    const uint64_t heads = __ballot(head) | ~__ballot(valid);  // an invalid lane also ends a run
-    if (head) {
-        const uint64_t after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-        const int next = after ? __builtin_ctzll(after) : 64;
-        atomicAdd(&hist[b], (uint32_t)(next - lane));
-    }
-    uint32_t m = v;
     const uint32_t nob = 0xFFFFFFFEu;
-    uint32_t pb = dpp_shr<1>(nob, b), pv = dpp_shr<1>(0u, m);
-    if (pb == b) m = max(m, pv);
-    pb = dpp_shr<2>(nob, b); pv = dpp_shr<2>(0u, m);
-    if (pb == b) m = max(m, pv);
-    pb = dpp_shr<4>(nob, b); pv = dpp_shr<4>(0u, m);
-    if (pb == b) m = max(m, pv);
-    pb = dpp_shr<8>(nob, b); pv = dpp_shr<8>(0u, m);
-    if (pb == b) m = max(m, pv);
-    // run tails from the ballot, like the heads: the next lane starts a run, holds no key or has left the
-    // caller's key loop (a shuffle from an inactive lane would read 0, i.e. bin 0: ADVICE r3)
-    const bool tail = valid && ((lane & 15) == 15 || lane == 63 || ((heads >> (lane + 1)) & 1ull));
-    if (tail) atomicMax(&bmax[b], m);
+    int cnt[NB];
+    uint32_t mx[NB];
+    bool tl[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const uint32_t b = bb[u];
+        const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
+        const bool valid = b != 0xFFFFFFFFu;
+        const bool head = valid && (lane == 0 || prev != b);
+        const uint64_t heads = __ballot(head) | ~__ballot(valid);  // an invalid lane also ends a run
+        const uint64_t after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+        cnt[u] = head ? (after ? __builtin_ctzll(after) : 64) - lane : 0;
+        uint32_t m = vv[u];
+        uint32_t pb = dpp_shr<1>(nob, b), pv = dpp_shr<1>(0u, m);
+        if (pb == b) m = max(m, pv);
+        pb = dpp_shr<2>(nob, b); pv = dpp_shr<2>(0u, m);
+        if (pb == b) m = max(m, pv);
+        pb = dpp_shr<4>(nob, b); pv = dpp_shr<4>(0u, m);
+        if (pb == b) m = max(m, pv);
+        pb = dpp_shr<8>(nob, b); pv = dpp_shr<8>(0u, m);
+        if (pb == b) m = max(m, pv);
+        mx[u] = m;
+        // run tails from the ballot, like the heads: the next lane starts a run, holds no key or has left the
+        // caller's key loop (a shuffle from an inactive lane would read 0, i.e. bin 0: ADVICE r3)
+        tl[u] = valid && ((lane & 15) == 15 || lane == 63 || ((heads >> (lane + 1)) & 1ull));
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        if (cnt[u]) atomicAdd(&hist[bb[u]], (uint32_t)cnt[u]);
+        if (tl[u]) atomicMax(&bmax[bb[u]], mx[u]);
+    }
 }
 
 struct ObLds {
@@ -1799,7 +1810,7 @@ struct ObLds {
     uint8_t* proc;
     uint32_t* tab;         // the level's X then Y table
     uint32_t* bmax;        // per bin: max of (response << 24 | 0xFFFFFF - key index)
-    uint16_t* bcell;       // per 64-key block: the cell of its first key (the first oct_kblk_max blocks)
+    uint16_t* bcell;       // per key block (kObKblkSh): the cell of its first key (the first oct_kblk_max blocks)
     uint64_t* lst2;        // FLAT: the second node list (packed code | (count << 8 | depth) << 32)
 };
 
@@ -1915,12 +1926,22 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         if (t == 0) *count_out = 0;
         return;
     }
-    // first cell of every 64-key block: the cells whose key range holds a multiple of 64 (keys past the
-    // table's Geo::oct_kblk_max blocks start from its last entry and walk further)
+    // every key's cell: a u16 per key in the node-list region (code0 .. proc, untouched until the passes)
+    // when the level's keys fit there (K <= kcap: every KITTI / EuRoC level); otherwise the first cell of
+    // every key block (the cells whose key range holds a multiple of 16; keys past the table's
+    // Geo::oct_kblk_max blocks start from its last entry), walked forward by the sweep
+    uint16_t* const kcell = (uint16_t*)d.code0;
+    const int kcap = (int)(((unsigned char*)d.tab - (unsigned char*)d.code0) >> 1);
+    const bool kdirect = K <= kcap;
     const int nblk = g.oct_kblk_max;
     for (int c = t; c < ncell; c += NT) {
         const int a = d.coff[c], e = d.coff[c + 1];
-        for (int b = (a + 63) >> 6; (b << 6) < e && b < nblk; ++b) d.bcell[b] = (uint16_t)c;
+        if (kdirect) {
+            for (int k = a; k < e; ++k) kcell[k] = (uint16_t)c;
+        } else {
+            for (int b = (a + (1 << kObKblkSh) - 1) >> kObKblkSh; (b << kObKblkSh) < e && b < nblk; ++b)
+                d.bcell[b] = (uint16_t)c;
+        }
     }
     __syncthreads();
     const uint32_t* islots = slots + (int64_t)img * g.slot_total;
@@ -1931,37 +1952,11 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         const int y = min(max((int)((v >> 12) & 0xFFFu) - kBorder, 0), ny - 1);
         return X[x] | Y[y];
     };
-    // Every key once: keys k = tid, tid + nthr, ... (consecutive keys in consecutive lanes: coalesced slot
-    // reads), kObBatch of them in flight per thread; a key's cell is the cell of its 64-key block's first key
-    // (bcell) walked forward over the few cells the block spans.  fn(k, slot value, code) for k < K.
-    // the 1 024-thread (small-batch) form keeps twice as many loads in flight: a level-0 workgroup holds ~5 000
-    // keys, i.e. ~5 per thread, which then take one round trip instead of two
+    // The first sweep, every key once: keys k = t, t + NT, ... (consecutive keys in consecutive lanes:
+    // coalesced slot reads), OB of them per thread per round; a key's cell from kcell (or its block's first
+    // cell walked forward); the OB keys' codes and run heads / tails first, then their LDS atomics (one
+    // key's atomics would otherwise order the next key's table reads behind them)
     constexpr int OB = NT >= 1024 ? 2 * kObBatch : kObBatch;
-    auto for_keys = [&](int tid, int nthr, auto&& fn) {
-        for (int k0 = tid; k0 < K; k0 += nthr * OB) {
-            int lo[OB];
-#pragma unroll
-            for (int u = 0; u < OB; ++u) lo[u] = d.bcell[min(min(k0 + nthr * u, K - 1) >> 6, nblk - 1)];
-            bool more = true;
-            while (__ballot(more)) {
-                more = false;
-#pragma unroll
-                for (int u = 0; u < OB; ++u) {
-                    const bool f = d.coff[lo[u] + 1] <= k0 + nthr * u && k0 + nthr * u < K;
-                    lo[u] += f;
-                    more |= f;
-                }
-            }
-            uint32_t v[OB];
-#pragma unroll
-            for (int u = 0; u < OB; ++u) {
-                const int k = k0 + nthr * u;
-                v[u] = k < K ? islots[d.soff[lo[u]] + (k - d.coff[lo[u]])] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < OB; ++u) fn(k0 + nthr * u, v[u], key_code(v[u]));
-        }
-    };
     // the first sweep also leaves every key's slot value in key order in global scratch (kc, the level's
     // 16-byte aligned range of the handle's candidate scratch), so the later sweeps (children of nodes
     // deeper than D0, the final map) read keys with dwordx4 loads instead of walking cells: for_cached,
@@ -1989,10 +1984,40 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         }
     };
     mark(5);
-    for_keys(t, NT, [&](int k, uint32_t v, uint32_t cd) {
-        bin_add_runs(d.bins, d.bmax, k < K ? cd >> bsh : 0xFFFFFFFFu, (v & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k));
-        if (k < K) kc[k] = v;
-    });
+    for (int k0 = t; k0 < K; k0 += NT * OB) {
+        int lo[OB];
+        if (kdirect) {
+#pragma unroll
+            for (int u = 0; u < OB; ++u) lo[u] = kcell[min(k0 + NT * u, K - 1)];
+        } else {
+#pragma unroll
+            for (int u = 0; u < OB; ++u) lo[u] = d.bcell[min(min(k0 + NT * u, K - 1) >> kObKblkSh, nblk - 1)];
+            bool more = true;
+            while (__ballot(more)) {
+                more = false;
+#pragma unroll
+                for (int u = 0; u < OB; ++u) {
+                    const bool f = d.coff[lo[u] + 1] <= k0 + NT * u && k0 + NT * u < K;
+                    lo[u] += f;
+                    more |= f;
+                }
+            }
+        }
+        uint32_t v[OB], bn[OB], bv[OB];
+#pragma unroll
+        for (int u = 0; u < OB; ++u) {
+            const int k = k0 + NT * u;
+            v[u] = k < K ? islots[d.soff[lo[u]] + (k - d.coff[lo[u]])] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < OB; ++u) {
+            const int k = k0 + NT * u;
+            bn[u] = k < K ? key_code(v[u]) >> bsh : 0xFFFFFFFFu;
+            bv[u] = (v[u] & 0xFF000000u) | (0xFFFFFFu - (uint32_t)k);
+            if (k < K) kc[k] = v[u];
+        }
+        bin_add_runs<OB>(d.bins, d.bmax, bn, bv);
+    }
     mark(6);
     __syncthreads();
     mark(1);
