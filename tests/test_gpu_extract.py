@@ -184,6 +184,24 @@ def test_extractor_configurations_bit_exact(ci):
     assert np.array_equal(desc, odesc), f"{params}: descriptors differ"
 
 
+def test_octree_key_walk_fallback():
+    """k_octree_bins keeps every key's cell in the node-list LDS when the level's keys fit (about 2 800 at
+    nfeatures = 100: 25-node lists); the noise image's level 0 holds far more, so its first sweep walks each
+    key's cell from its 16-key block's first cell instead.  Both paths must select the reference's keys."""
+    rng = np.random.default_rng(21)
+    img = rng.integers(0, 256, (376, 1241)).astype(np.uint8)
+    params = dict(KITTI, nfeatures=100)
+    ex = ORBextractor(**params)
+    kps, desc = ex.extract(img)
+    assert len(_debug(ex, "orbfe_debug_candidates", 0)) > 8000
+    okps, odesc = O.OracleExtractor(**params).extract(img)
+    assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
+    npl = ex.features_per_level()
+    cand = _debug(ex, "orbfe_debug_candidates", 0)
+    exp = O.octree(cand, 16, 1241 - 16, 16, 376 - 16, npl[0])
+    assert np.array_equal(_debug(ex, "orbfe_debug_selected", 0), exp)
+
+
 def test_strided_view_input_follows_the_reference_caster():
     """A sliced ROI view is read as nh x nw consecutive bytes from its first element (the reference caster
     ignores strides, opencv_type_casters.h:200): the drop-in's result equals the oracle's on those bytes and
