@@ -2234,30 +2234,53 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         uint64_t* nxt = d.lst2;
         // the list after pass J: depth J (every created node), then depths J-1 .. 0 (single-key nodes)
         {
-            int v[EP], dk[EP], ik[EP];
+            // every entry's depth from one scalar walk over the depths (not one per entry), then all entries'
+            // bin reads issued together (clamped, unconditional) and waited once: per-entry branches had
+            // serialised the entries' LDS round trips
+            const int nini = __builtin_amdgcn_readfirstlane(L.n_ini);
+            int v[EP], dk[EP], ik[EP], rr[EP];
 #pragma unroll
             for (int k = 0; k < EP; ++k) {
-                const int f = t * EP + k;
-                int o = 0, dd = -1, r = 0;
+                dk[k] = -1;
+                rr[k] = 0;
+            }
+            {
+                int o = 0;
                 for (int e = J; e >= 0; --e) {
-                    const int P = L.n_ini << (2 * e);
-                    if (dd < 0 && f < o + P) {
-                        dd = e;
-                        r = f - o;
+                    const int P = nini << (2 * e);
+#pragma unroll
+                    for (int k = 0; k < EP; ++k) {
+                        const int f = t * EP + k;
+                        if (dk[k] < 0 && f < o + P) {
+                            dk[k] = e;
+                            rr[k] = f - o;
+                        }
                     }
                     o += P;
                 }
-                int i = 0, c = 0, pc = 2;
-                if (dd >= 0) {
-                    const int sh = 2 * dd;
-                    const int colp = r >> sh;
-                    const int col = (dd & 1) ? L.n_ini - 1 - colp : colp;
-                    i = (col << sh) | ((r & ((1 << sh) - 1)) ^ (0x33333333 & ((1 << sh) - 1)));
-                    c = ncnt(dd, i);
-                    if (dd) pc = ncnt(dd - 1, i >> 2);
-                }
-                dk[k] = dd;
+            }
+            int a0[EP], a1[EP], b0[EP], b1[EP];
+#pragma unroll
+            for (int k = 0; k < EP; ++k) {
+                const int dd = max(dk[k], 0), sh = 2 * dd, r = rr[k];
+                const int colp = r >> sh;
+                const int col = (dd & 1) ? nini - 1 - colp : colp;
+                const int i = (col << sh) | ((r & ((1 << sh) - 1)) ^ (0x33333333 & ((1 << sh) - 1)));
                 ik[k] = i;
+                const int bs = 2 * (D0 - dd);  // ncnt(dd, i) and, below, ncnt(dd - 1, i >> 2)
+                a0[k] = (int)d.bins[i << bs];
+                a1[k] = (int)d.bins[(i + 1) << bs];
+                const int pi = dd ? i >> 2 : 0, ps = dd ? bs + 2 : bs;
+                b0[k] = (int)d.bins[pi << ps];
+                b1[k] = (int)d.bins[(pi + 1) << ps];
+            }
+            int cc[EP];
+#pragma unroll
+            for (int k = 0; k < EP; ++k) {
+                const int dd = dk[k];
+                const int c = (a1[k] & ~(int)kObDeep) - (a0[k] & ~(int)kObDeep);
+                const int pc = dd > 0 ? (b1[k] & ~(int)kObDeep) - (b0[k] & ~(int)kObDeep) : 2;
+                cc[k] = c;
                 v[k] = dd >= 0 && c >= 1 && pc >= 2 && (dd == J || c == 1);
             }
             int fl[EP];
@@ -2266,7 +2289,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
             bscan(v);
 #pragma unroll
             for (int k = 0; k < EP; ++k)
-                if (fl[k] && v[k] < CAPL) cur[v[k]] = pack((uint32_t)ik[k] << (2 * (D - dk[k])), ncnt(dk[k], ik[k]), dk[k]);
+                if (fl[k] && v[k] < CAPL) cur[v[k]] = pack((uint32_t)ik[k] << (2 * (D - dk[k])), cc[k], dk[k]);
         }
         if (S > CAPL) {  // cannot happen (S <= N or <= 4 nIni, both within kp_cap <= CAPL)
             if (t == 0) atomicOr(overflow, 4);
