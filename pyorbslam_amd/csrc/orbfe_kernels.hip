@@ -2881,7 +2881,14 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         uint32_t m = 0u;
         if (dp <= D0) {
             const int w = 1 << (2 * (D0 - dp));
-            for (int b = lo; b < lo + w; ++b) m = max(m, d.bmax[b]);
+            if (w == 1) {
+                m = d.bmax[lo];
+            } else {  // w a power of 4 and lo a multiple of w: 16-byte aligned runs of 4 bins
+                for (int b = lo; b < lo + w; b += 4) {
+                    const uint4 q = *(const uint4*)(d.bmax + b);
+                    m = max(m, max(max(q.x, q.y), max(q.z, q.w)));
+                }
+            }
         }
         best[p] = m;
     }
@@ -2906,12 +2913,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
         const uint32_t bv = best[p];
         const int k = 0xFFFFFF - (int)(bv & 0xFFFFFFu);
         if (bv != 0u && k < K) {
-            int lo = 0, hi = ncell - 1;  // last cell with coff <= k
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (d.coff[mid] <= k) lo = mid; else hi = mid - 1;
-            }
-            out[p] = islots[d.soff[lo] + (k - d.coff[lo])];
+            out[p] = kc[k];  // the first sweep's copy of the key's slot value (no binary search over the cells)
         } else {  // a node without keys cannot occur; flag instead of reading out of range
             out[p] = 0u;
             atomicOr(overflow, 16);
