@@ -1955,8 +1955,9 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     // The first sweep, every key once: keys k = t, t + NT, ... (consecutive keys in consecutive lanes:
     // coalesced slot reads), OB of them per thread per round; a key's cell from kcell (or its block's first
     // cell walked forward); the OB keys' codes and run heads / tails first, then their LDS atomics (one
-    // key's atomics would otherwise order the next key's table reads behind them)
-    constexpr int OB = NT >= 1024 ? 2 * kObBatch : kObBatch;
+    // key's atomics would otherwise order the next key's table reads behind them).  OB: 4 at 256 threads, 2 at
+    // 512 (small batches: 8 pairs 30.3 -> 29.2 us; 4 / 8 at 256 threads: 0.358 / 0.371 ms standalone)
+    constexpr int OB = NT >= 512 ? kObBatch / 2 : kObBatch;
     // the first sweep also leaves every key's slot value in key order in global scratch (kc, the level's
     // 16-byte aligned range of the handle's candidate scratch), so the later sweeps (children of nodes
     // deeper than D0, the final map) read keys with dwordx4 loads instead of walking cells: for_cached,
