@@ -234,7 +234,11 @@ int orbfe_batch_status(orbfe_handle h, int32_t* overflow);
  * pairs [pair0, pair0 + n_pairs) of the last stereo batch to d_records (n_pairs x rec_bytes, 4-byte
  * aligned) on hip_stream, without synchronising.  d_records is device memory or page-locked host memory
  * (hipHostMalloc): the records then go over PCIe straight into host memory (no device staging buffer, no
- * copy-engine transfer); pageable memory is refused with ORBFE_EINVAL. */
+ * copy-engine transfer); pageable memory is refused with ORBFE_EINVAL.
+ * Ordering (both pack calls): on the batch's own stream the pack simply follows it.  On another stream the
+ * pack waits on an event recorded on the batch's stream WHEN THE PACK IS CALLED, so (a) that stream must
+ * still exist and must not be inside a graph capture at that moment, and (b) whatever was queued on it after
+ * the batch and before the pack call is waited for too. */
 int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes);
 /* Compact records (the host-fed D2H leg and the rank-0 gather, 25 % smaller): counts L, R (2 x i32) |
  * keypoints L, R (kp_cap x {u32 x | y << 12 | octave << 24 in the keypoint's level pixels, f32 angle}) |

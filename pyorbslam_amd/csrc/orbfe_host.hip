@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -747,15 +748,18 @@ constexpr int kCascadeImages = kSmallBatchImages;
 
 // compute units of the current device (one strip workgroup per CU: a 1 024-thread strip is a latency chain,
 // and two of them on one CU run at half speed each)
+// (atomic entries: handles on several threads may ask at once; a race only repeats the same query)
 static int device_cus() {
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int v = 0;
-        cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    int v = cus[dev].load(std::memory_order_relaxed);
+    if (!v) {
+        int a = 0;
+        v = hipDeviceGetAttribute(&a, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && a > 0 ? a : 256;
+        cus[dev].store(v, std::memory_order_relaxed);
     }
-    return cus[dev];
+    return v;
 }
 
 // strips per image: at most one workgroup per CU for the batch (8 images on 256 CUs: 32 strips, not 35 of which

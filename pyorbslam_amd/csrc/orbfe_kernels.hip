@@ -3057,11 +3057,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // octree's level keypoints only, stereo_bucket_pair): dispatched first, they run under the descriptor
     // workgroups instead of as a launch of their own after them (the host fuses only when H + 1 counters fit
     // s_h and the block is 256 threads)
-    if ((int)blockIdx.x < n_bucket) {
-        if constexpr (WAVES == 4) stereo_bucket_pair<256>(g, sa, blockIdx.x, (int*)&s_h[0][0], (int*)&s_src[0][0]);
+    // n_lead: the bucket workgroups rounded up to a multiple of 8 (the extra ones return at once), so that the
+    // descriptor workgroups' hw & 7 below is still their XCD
+    const int n_lead = (n_bucket + 7) & ~7;
+    if ((int)blockIdx.x < n_lead) {
+        if constexpr (WAVES == 4)
+            if ((int)blockIdx.x < n_bucket) stereo_bucket_pair<256>(g, sa, blockIdx.x, (int*)&s_h[0][0], (int*)&s_src[0][0]);
         return;
     }
-    const int nb = (int)gridDim.x - n_bucket, hw = (int)blockIdx.x - n_bucket;  // 1-D grid: n_bucket + gx images
+    const int nb = (int)gridDim.x - n_lead, hw = (int)blockIdx.x - n_lead;  // 1-D grid: n_lead + gx images
     const int per = nb >> 3;
     const int lb = hw < 8 * per ? (hw & 7) * per + (hw >> 3) : hw;  // XCD-aware: runs of waves per L2
     const int img = __builtin_amdgcn_readfirstlane(lb / gx);
@@ -4096,7 +4100,7 @@ static void launch_orb_nw(const Geo& g, const uint8_t* in, int64_t in_pitch, con
     const int waves = orb_waves(g, KPW);  // most waves an image can need: KPW keypoints per wave, per level
     const int gx = (waves + NW - 1) / NW;
     const int nbk = bucket && NW == 4 ? n_bucket : 0;
-    hipLaunchKernelGGL((k_orb<NW, KPW>), dim3(nbk + gx * n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws, lvl_kp,
+    hipLaunchKernelGGL((k_orb<NW, KPW>), dim3(((nbk + 7) & ~7) + gx * n_images), dim3(64 * NW), 0, s, g, in, in_pitch, ws, lvl_kp,
                        lvl_count, out_kp, out_desc, out_count, tab, gx, bucket ? *bucket : StereoArgs{}, nbk);
 }
 

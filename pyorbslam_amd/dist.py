@@ -8,6 +8,7 @@ gloo on CPU): `pack_device` builds the records on the GPU with k_pack, `gather_r
 """
 from __future__ import annotations
 
+import hashlib
 import time
 
 import numpy as np
@@ -192,12 +193,74 @@ def pack_device(frontends, counts, out, compact: bool = False) -> None:
         o += n
 
 
+def fields_digest(kl, dl, kr, dr, stereo: dict) -> bytes:
+    """SHA-256 over one pair's result fields in record order — keypoints L, R (orbfe_keypoint records),
+    descriptors L, R, u_right, depth, status — as orbfe_batch_fetch / _fetch_stereo return them and as
+    unpack / unpack_compact rebuild them from a gathered record.  Equal digests = every field bit-equal."""
+    h = hashlib.sha256()
+    for a in (kl, kr, dl, dr, stereo["u_right"], stereo["depth"], stereo["status"]):
+        a = np.ascontiguousarray(a)
+        h.update(np.int64(a.size).tobytes())
+        h.update(a.tobytes())
+    return h.digest()
+
+
+DIGEST_ROW = 33  # per sent record: valid flag (1 B) + fields_digest (32 B); padded rows send zeros
+
+
+def local_digests(frontends, counts, max_local: int) -> np.ndarray:
+    """(max_local, DIGEST_ROW) uint8: row j = 1 + fields_digest of this rank's local pair j (handle-major, the
+    order pack_device writes), fetched through orbfe_batch_fetch / orbfe_batch_fetch_stereo — independent of
+    k_pack; rows past the rank's own pairs (padding of uneven shards) stay zero."""
+    out = np.zeros((int(max_local), DIGEST_ROW), np.uint8)
+    j = 0
+    for f, n in zip(frontends, counts):
+        for p in range(int(n)):
+            kl, dl = f.fetch_image(2 * p)
+            kr, dr = f.fetch_image(2 * p + 1)
+            out[j, 0] = 1
+            out[j, 1:] = np.frombuffer(fields_digest(kl, dl, kr, dr, f.fetch_stereo(p)), np.uint8)
+            j += 1
+    return out
+
+
+def check_gathered(full: np.ndarray, digests: np.ndarray, unpack_fn) -> dict:
+    """Rank 0's check of a gather: full (world * max_local, record_bytes) records in rank-major order,
+    digests (world * max_local, DIGEST_ROW) the senders' local_digests in the same order.  Every valid row is
+    unpacked (unpack_fn(record) -> unpack()'s dict) and its fields' digest compared with its sender's; every
+    padded row must be all zero bytes.  Returns counts and the first failing rows (rank, local index)."""
+    full = np.asarray(full)
+    digests = np.asarray(digests)
+    if full.shape[0] != digests.shape[0]:
+        raise ValueError("records and digests disagree in row count")
+    verified, padded, bad = 0, 0, []
+    for i in range(full.shape[0]):
+        if digests[i, 0]:
+            u = unpack_fn(full[i])
+            d = fields_digest(u["kps_left"], u["desc_left"], u["kps_right"], u["desc_right"], u)
+            if d == digests[i, 1:].tobytes():
+                verified += 1
+            else:
+                bad.append(i)
+        elif digests[i].any() or full[i].any():
+            bad.append(i)
+        else:
+            padded += 1
+    return {"ok": not bad, "records_verified": verified, "padded_rows_zero": padded, "bad_rows": bad[:8],
+            "rows": int(full.shape[0])}
+
+
 def timed_gather(frontends, counts, device, world: int, rank: int, max_local: int | None = None,
                  reps: int = 3, compact: bool = True) -> dict:
     """Pack (k_pack_compact: compact records, 25 % fewer bytes over xGMI) + gather to rank 0 of every pair's
     results, timed like the bench step (barrier + synchronise on both sides, max over ranks); every rank
-    sends max_local records (its own pairs, padded: uneven shards of a strong-scaling run).  The records of
-    rank 0's own first pair are checked against orbfe_batch_fetch."""
+    sends max_local records (its own pairs, padded: uneven shards of a strong-scaling run).
+
+    Then, untimed, EVERY gathered row is checked: each rank sends, in a second gather,
+    the digest of each of its pairs' fields as orbfe_batch_fetch / _fetch_stereo return them (local_digests,
+    independent of k_pack); rank 0 unpacks every record and compares its fields' digest with its sender's,
+    and checks that the padded rows of uneven shards are zero (check_gathered).  Rank 0's own first pair is
+    also compared field by field."""
     import torch
     import torch.distributed as dist
     n_local = int(sum(counts))
@@ -205,6 +268,7 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
     kc = frontends[0].kp_cap
     rb = compact_record_bytes(kc) if compact else record_bytes(kc)
     buf = torch.zeros((max_local, rb), dtype=torch.uint8, device=device)
+    nccl = world > 1 and dist.get_backend() == "nccl"
     times = []
     full = None
     for _ in range(reps + 1):
@@ -214,7 +278,7 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
         t0 = time.perf_counter()
         pack_device(frontends, counts, buf, compact)
         # RCCL gathers the device buffer in place; a gloo rehearsal (several ranks on one GPU) stages it
-        src = buf if world == 1 or dist.get_backend() == "nccl" else buf.cpu()
+        src = buf if world == 1 or nccl else buf.cpu()
         # the one receive buffer of this shape, reused across the repetitions (allocated outside the timing
         # by the warm-up repetition)
         full = gather_records(src, 0, out=gather_buffer(world, src) if rank == 0 and world > 1 else None)
@@ -224,25 +288,35 @@ def timed_gather(frontends, counts, device, world: int, rank: int, max_local: in
         times.append(time.perf_counter() - t0)
     dt = float(np.mean(times[1:]))
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=device if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ok = None
+    # untimed: every rank's digests to rank 0 (same collective path as the records)
+    dg = torch.from_numpy(local_digests(frontends, counts, max_local))
+    dg_full = gather_records(dg.to(device) if nccl else dg, 0) if world > 1 else dg
+    ok, chk = None, None
     if rank == 0:
-        rec0 = full[0].cpu().numpy()
-        u = unpack_compact(kc, rec0, frontends[0].scales) if compact else unpack(kc, rec0)
+        full_np = full.cpu().numpy() if world > 1 else buf.cpu().numpy()
+        unpack_fn = ((lambda r: unpack_compact(kc, r, frontends[0].scales)) if compact else (lambda r: unpack(kc, r)))
+        chk = check_gathered(full_np, dg_full.cpu().numpy(), unpack_fn)
+        u = unpack_fn(full_np[0])
         k, d = frontends[0].fetch_image(0)
         kr, dr = frontends[0].fetch_image(1)
         s = frontends[0].fetch_stereo(0)
-        ok = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
-              and u["kps_right"].tobytes() == kr.tobytes() and np.array_equal(u["desc_right"], dr)
-              and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["depth"], s["depth"])
-              and np.array_equal(u["status"], s["status"]))
+        first = (u["kps_left"].tobytes() == k.tobytes() and np.array_equal(u["desc_left"], d)
+                 and u["kps_right"].tobytes() == kr.tobytes() and np.array_equal(u["desc_right"], dr)
+                 and np.array_equal(u["u_right"], s["u_right"]) and np.array_equal(u["depth"], s["depth"])
+                 and np.array_equal(u["status"], s["status"]))
+        ok = bool(first and chk["ok"])
         if not ok:
-            raise RuntimeError("gathered record of pair 0 differs from orbfe_batch_fetch")
+            raise RuntimeError(f"gathered records differ from their senders' orbfe_batch_fetch results: {chk}")
     return {"gather_ms": round(1e3 * dt, 4), "record_bytes": rb, "records": "compact" if compact else "full",
             "pairs_gathered": world * max_local,
+            "records_verified": chk["records_verified"] if chk else None,
+            "padded_rows_zero": chk["padded_rows_zero"] if chk else None,
             "bytes_to_rank0": world * max_local * rb, "record_check": ok,
             "GBs_into_rank0": round(world * max_local * rb / dt / 1e9, 2),
             "what": "k_pack on every rank + one gather of the records to rank 0 (RCCL with nccl, gloo on CPU), "
-                    f"mean of {reps} after 1 warm-up, barrier + synchronize around each, max over ranks"}
+                    f"mean of {reps} after 1 warm-up, barrier + synchronize around each, max over ranks; then every "
+                    "gathered record unpacked on rank 0 and checked against its sender's fetched-field digest, "
+                    "padded rows checked zero"}

@@ -314,6 +314,10 @@ class ORBextractor:
         # want_pyramid: the sheared views stay on the device until read (2, lazy); False: built on request
         call("orbfe_frame_extract", self._h, ptr(L), ptr(R), w, h, w, float(mbf), float(np.float32(fx32)),
              2 if want_pyramid else 0)
+        if w > 0 and h > 0 and self._frame_shapes is None:
+            # the level sizes now, while orbfe_frame_pyramid answers (it needs this handle's last call to be a
+            # frame): a lazy list read after a plain extract() on this handle still finds them
+            self._level_shapes(0)
         serial = C.c_int64()
         call("orbfe_frame_serial", self._h, C.byref(serial), None)
         lazy = bool(want_pyramid)

@@ -27,7 +27,10 @@ def test_bench_two_ranks_through_the_launcher():
     assert out["parity_failures"] == 0 and out["overflow"] == 0 and out["parity_checked_pairs"] == 16
     assert out["with_gather"]["record_check"] is True
     assert out["with_gather"]["pairs_gathered"] == 16
+    # every gathered record unpacked on rank 0 and checked against its sender's digest
+    assert out["with_gather"]["records_verified"] == 16
     assert out["c4_strong"]["with_gather"]["record_check"] is True
+    assert out["c4_strong"]["with_gather"]["records_verified"] == 64
     assert out["c4_strong"]["pairs_per_gpu"] == 32
     assert out["host_fed"]["record_check"] is True
 
@@ -49,4 +52,6 @@ def test_c4_eight_ranks_through_the_launcher():
     assert out["parity_failures"] == 0 and out["overflow"] == 0 and out["parity_checked_pairs"] == 64
     g = out["c4_strong"]["with_gather"]
     assert g["record_check"] is True and g["pairs_gathered"] == 64
+    assert g["records_verified"] == 64 and g["padded_rows_zero"] == 0
+    assert out["with_gather"]["record_check"] is True and out["with_gather"]["records_verified"] == 64
     assert out["with_gather"]["bytes_to_rank0"] == 64 * g["record_bytes"]

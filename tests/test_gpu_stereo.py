@@ -419,6 +419,32 @@ def test_right_extractor_keeps_its_pyramid_after_the_left_moves_on():
         assert np.array_equal(g_, w_)
 
 
+@pytest.mark.parametrize("resize_first", [False, True])
+def test_lazy_pyramid_first_read_after_a_plain_extract(resize_first):
+    """a lazy frame's pyramids first read only after the left extractor ran a plain
+    extract() — at the frame's size (the handle's last call is then no frame) or at another size (which clears
+    the device ring, so every unread list is fetched first).  Both extractors' lists, and a Frame-style list
+    taken before, still equal the oracle's sheared views of their own images."""
+    from oracle.oracle import OracleExtractor
+    L1, R1 = synth.make_pair(31, 641, 333)
+    prm = dict(KITTI, nfeatures=700)
+    left, rA = ORBextractor(**prm), ORBextractor(**prm)
+    o = OracleExtractor(**prm)
+    left.operator_kd_stereo(L1, R1, rA, BF, np.float32(FX))
+    taken_left = left.GetImagePyramid()
+    other = synth.make_pair(32, 500, 300)[0] if resize_first else L1
+    left.extract(other)
+    o.extract(R1)
+    for g_, w_ in zip(rA.GetImagePyramid(), o.sheared_pyramid()):
+        assert np.array_equal(g_, w_)
+    o.extract(L1)
+    for g_, w_ in zip(taken_left, o.sheared_pyramid()):
+        assert np.array_equal(g_, w_)
+    o.extract(other)
+    for g_, w_ in zip(left.GetImagePyramid(), o.sheared_pyramid()):
+        assert np.array_equal(g_, w_)
+
+
 def test_lazy_frame_pyramids_ring():
     """the frame path's sheared pyramids stay in a device ring (ORBFE_FRAME_RING frames) and
     cross PCIe only when read.  Lists read late, copied lazily (Frame.copy) or forced out by the ring's
