@@ -40,6 +40,7 @@ from __future__ import annotations
 import argparse
 import ctypes as C
 import json
+import math
 import os
 import socket
 import subprocess
@@ -142,6 +143,36 @@ def _cpu_worker(seeds, width, height, nfeatures, barrier, queue):
     return len(pairs), dt, t_ext
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the job's cgroup may use (cgroup v2 cpu.max, v1 cfs quota), None when unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def job_cpus() -> dict:
+    """The host cores this job has: the CPUs in its affinity mask, capped by its cgroup's
+    CPU quota when there is one — on the GPU box the mask holds all 256 hardware threads of the machine but
+    cpu.max grants 16 CPUs' worth of time, so more processes than that only share those 16 (measured:
+    profiles/r06/cpu_baseline_procs_r6.log)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    cores = max(1, min(aff, int(math.ceil(quota))) if quota else aff)
+    return {"cores": cores, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "cores_rule": "min(affinity CPUs, cgroup CPU quota)"}
+
+
 def cpu_baseline(sample_pairs: int, width: int, height: int, nfeatures: int, procs: int):
     """1 thread on `sample_pairs` pairs, then `procs` independent processes with 4 pairs each (all the
     host cores this job may use).  Runs BEFORE anything initialises the GPU (the pool forks)."""
@@ -220,7 +251,7 @@ def parity_check(fes, counts, host, width, height, nfeatures, pairs_total=64, ca
                 return f"handle {hi} pair {p}: stereo differs from the restatement"
         return None
 
-    workers = max(1, min(16, len(os.sched_getaffinity(0))))  # the box's CPU share for one GPU
+    workers = job_cpus()["cores"]  # the job's host cores (affinity capped by the cgroup CPU quota)
     with ThreadPoolExecutor(workers) as ex:
         bad = [r for r in ex.map(check, jobs) if r is not None]
     return len(jobs), ovf, bad
@@ -689,8 +720,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=1, help="internal concurrent chunks per handle (orbfe_set_lanes)")
     ap.add_argument("--cpu-sample", type=int, default=40,
                     help="pairs timed on 1 thread for cpu_baseline (0 = skip); the all-cores figure adds 4 per process")
-    ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = this "
-                    "job's CPU share, at most 16)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="processes for the all-cores cpu_baseline (0 = the job's "
+                    "host cores: its affinity CPUs capped by its cgroup CPU quota, job_cpus)")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity check of the bench workload")
     ap.add_argument("--parity-pairs", type=int, default=64,
                     help="pairs of the timed batch checked against the oracle after the timed region (per rank)")
@@ -738,12 +769,10 @@ def main():
     extras = not args.roofline_only
     cpu = None
     if world == 1 and args.cpu_sample > 0 and extras:
-        try:
-            share = len(os.sched_getaffinity(0))
-        except AttributeError:  # pragma: no cover
-            share = os.cpu_count() or 1
-        procs = args.cpu_procs or max(1, min(16, share))
+        cpus = job_cpus()
+        procs = args.cpu_procs or cpus["cores"]
         cpu = cpu_baseline(args.cpu_sample, args.width, args.height, args.nfeatures, procs)
+        cpu.update({k: v for k, v in cpus.items() if k != "cores"})
 
     import torch
     import torch.distributed as dist

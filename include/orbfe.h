@@ -32,7 +32,8 @@ extern "C" {
 /* ABI revision of this header (orbfe_abi_version() returns the library's).  4: ORBFE_NSTAGES = 5 (stage 3
  * describe, 4 stereo; the round-1 blur stage and orbfe_set_blur_fork are gone), orbfe_set_graphs,
  * orbfe_set_octree_kernel / orbfe_get_octree_kernel, orbfe_debug_detect_stats. */
-#define ORBFE_ABI_VERSION 5
+#define ORBFE_ABI_VERSION 6 /* 6: compact gather records pack x | y << 14 | octave << 28 (was 12 / 12 / 24); level
+                               * sides above 4 095 px are accepted (kKeyXYBits) */
 /* frames whose sheared pyramids the lazy frame path (want_pyramid = 2) keeps on the device */
 #define ORBFE_FRAME_RING 8
 int32_t orbfe_abi_version(void);
@@ -241,7 +242,7 @@ int orbfe_batch_status(orbfe_handle h, int32_t* overflow);
  * the batch and before the pack call is waited for too. */
 int orbfe_batch_record_bytes(orbfe_handle h, int64_t* bytes);
 /* Compact records (the host-fed D2H leg and the rank-0 gather, 25 % smaller): counts L, R (2 x i32) |
- * keypoints L, R (kp_cap x {u32 x | y << 12 | octave << 24 in the keypoint's level pixels, f32 angle}) |
+ * keypoints L, R (kp_cap x {u32 x | y << 14 | octave << 28 in the keypoint's level pixels, f32 angle}) |
  * descriptors L, R (kp_cap x 32 B) | u_right, depth (kp_cap x f32) | FAST scores L, R (kp_cap x u8) | status
  * (kp_cap x i8), padded to 16 bytes (8 + 91 kp_cap).  The keypoint tuples follow exactly: x = f32(level x) *
  * scale[octave] (ORBextractor.cpp:1094-1099), size = (float)(int)(31 * scale[octave]), response = score

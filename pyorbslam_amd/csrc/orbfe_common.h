@@ -16,7 +16,14 @@ constexpr int kBorder = kEdge - 3; // minBorderX/Y (ORBextractor.cpp:772-773)
 constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
 constexpr int kPatchR = 21;        // descriptor patch radius: 18 (max rotated pattern offset) + 3 (blur)
 constexpr int kPatchD = 2 * kPatchR + 1;  // 43
-constexpr int kMaxLevelSide = 4095;  // level coordinates are 12-bit fields (FAST slots, level keypoints, compact records)
+// Level coordinates in the FAST slots, the octree's key cache and the level keypoints are packed as
+// (x + y * w) | score << 24 with w the level's width: the pixel's row-major index in 24 bits, so every level
+// of at most 2^24 pixels (4 096 x 4 096, 4 500 x 2 300, 2 500 x 4 500, ...) fits, whatever its aspect.  Decoding
+// divides by w with a per-level magic multiplier (LevelGeo::kmag, ksh; key_xy in the kernels).
+constexpr int kKeyXYBits = 24;
+constexpr int kMaxCellCoord = 32767;  // CellGeo's int16 ROI coordinates (and its int16 level width)
+// compact gather records (k_pack_compact): x | y << 14 | octave << 28, levels up to 16 383 px per side
+constexpr int kCompactXYBits = 14;
 constexpr int kMaxCellRoi = 64;    // max cell ROI side (wCell+6, hCell+6); checked on the host
 
 // One pyramid level of one image geometry.
@@ -54,11 +61,14 @@ struct LevelGeo {
     // quadrant).  Candidates are counted per depth-oct_d0 node (oct_bins bins, column-major).
     int oct_d, oct_d0, oct_bins;
     int oct_xt, oct_yt, oct_nx, oct_ny;
+    // packed level keys (kKeyXYBits): y = mul_hi(xy, kmag) >> ksh, x = xy - y * w for xy < 2^24
+    uint32_t kmag;
+    int ksh;
 };
 
 // One FAST cell (ORBextractor.cpp:788-828): ROI rows [y0,y1), cols [x0,x1) in level coordinates.
 struct CellGeo {
-    int16_t level, pad;
+    int16_t level, kw;   // kw: the level's width, the radix of its packed keys (k_detect, kKeyXYBits)
     int16_t x0, y0, x1, y1;
     int slot_off;        // offset (in keys) of the cell's output slot inside an image's slot array
     int slot_cap;        // ceil(ww/2)*ceil(wh/2): strict 3x3 NMS keeps at most one pixel per 2x2 block

@@ -390,6 +390,35 @@ void octree_tables(LevelGeo& L, int n_feat, std::vector<uint32_t>& tab) {
     }
 }
 
+// The divisor of a level's packed keys (kKeyXYBits, key_xy in the kernels): y = mul_hi(xy, kmag) >> ksh ==
+// floor(xy / w) for every xy < 2^24 with kmag = ceil(2^(31 + s) / w), ksh = s - 1, s = ceil(log2 w) (kmag < 2^32
+// because w > 2^(s - 1); exact because the error term xy * (kmag * w - 2^(31 + s)) < 2^24 * w < 2^(31 + s)).
+// Checked here on the level's extreme and row-boundary indices.  A 1-px-wide level has no FAST cells, hence no
+// keys: its divisor only has to exist.
+void key_divisor(LevelGeo& L) {
+    const uint32_t w = (uint32_t)L.w;
+    if (w < 2) {
+        L.kmag = 0;
+        L.ksh = 0;
+        return;
+    }
+    int s = 0;
+    while ((1u << s) < w) ++s;
+    const unsigned __int128 num = (unsigned __int128)1 << (31 + s);
+    const uint64_t mag = (uint64_t)((num + w - 1) / w);
+    if (mag > 0xFFFFFFFFull) throw Error(ORBFE_EINVAL, "key divisor out of range");
+    L.kmag = (uint32_t)mag;
+    L.ksh = s - 1;
+    const uint32_t n = w * (uint32_t)L.h;
+    for (uint32_t y : {0u, 1u, (uint32_t)L.h / 2, (uint32_t)L.h - 1})
+        for (int64_t d : {(int64_t)-1, (int64_t)0, (int64_t)1, (int64_t)w - 1}) {
+            const int64_t v = (int64_t)y * w + d;
+            if (v < 0 || v >= (int64_t)n) continue;
+            const uint32_t q = (uint32_t)(((uint64_t)(uint32_t)v * L.kmag) >> 32) >> L.ksh;
+            if (q != (uint32_t)v / w) throw Error(ORBFE_EINVAL, "key divisor check failed");
+        }
+}
+
 void build_geometry(orbfe_ctx& c, int W, int H) {
     const int L = c.prm.nlevels;
     Geo& g = c.geo;
@@ -416,10 +445,14 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
         Lg.inv_scale = c.isf[l];
         Lg.w = round_even_f((float)W * c.isf[l]);
         Lg.h = round_even_f((float)H * c.isf[l]);
-        // kMaxLevelSide: the 12-bit level coordinates of the FAST slots, the level keypoints and the compact
-        // gather records (k_detect, k_octree_bins, k_pack_compact)
-        if (Lg.w < 1 || Lg.h < 1 || Lg.w > kMaxLevelSide || Lg.h > kMaxLevelSide)
-            throw Error(ORBFE_EINVAL, "level size out of range (1..4095 px per side)");
+        // the packed level keys (FAST slots, key cache, level keypoints: (x + y * w) | score << 24) hold a
+        // pixel's row-major index in 24 bits (kKeyXYBits): every level of at most 2^24 pixels
+        if (Lg.w < 1 || Lg.h < 1) throw Error(ORBFE_EINVAL, "level size out of range (empty level)");
+        if ((int64_t)Lg.w * Lg.h > (int64_t)1 << kKeyXYBits || Lg.w > kMaxCellCoord || Lg.h > kMaxCellCoord)
+            throw Error(ORBFE_EINVAL, "level " + std::to_string(l) + " (" + std::to_string(Lg.w) + "x" + std::to_string(Lg.h) +
+                                          ") has more than 2^24 pixels (or a side above 32 767 px): its pixel index does "
+                                          "not fit the 24 bits of a packed level key");
+        key_divisor(Lg);
         // levels of 19 px or less are padded by an iterated reflection (k_shear); they have no FAST cells
         Lg.pitch = (Lg.w + 15) & ~15;
         if (l > 0) {
@@ -454,6 +487,7 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
                     if (maxXc > maxX) maxXc = (float)maxX;
                     CellGeo cg{};
                     cg.level = (int16_t)l;
+                    cg.kw = (int16_t)Lg.w;
                     cg.x0 = (int16_t)(int)iniX;
                     cg.y0 = (int16_t)(int)iniY;
                     cg.x1 = (int16_t)(int)maxXc;
@@ -503,7 +537,10 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
             if (Lg.span_y <= 0 || Lg.span_x <= 0) throw Error(ORBFE_EINVAL, "degenerate level");
             Lg.n_ini = (int)std::round((float)Lg.span_x / Lg.span_y);
             if (Lg.n_ini <= 0)
-                throw Error(ORBFE_EINVAL, "level aspect ratio < 0.5: the reference octree indexes out of range");
+                throw Error(ORBFE_EINVAL, "level " + std::to_string(l) + " (" + std::to_string(Lg.w) + "x" +
+                                              std::to_string(Lg.h) + "): the reference's DistributeOctTree indexes "
+                                              "vpIniNodes out of range (nIni = round(spanX / spanY) = 0 with FAST cells, "
+                                              "ORBextractor.cpp:543-568)");
             Lg.hx = (float)Lg.span_x / Lg.n_ini;
         }
         Lg.kp_cap = std::max(Lg.n_feat + 2, 4 * Lg.n_ini) + 2;
@@ -1566,9 +1603,9 @@ int orbfe_batch_pack_compact_device(orbfe_handle h, uint8_t* d_records, int64_t 
         if (rec_bytes != compact_record_bytes(h->geo.kp_cap))
             throw Error(ORBFE_EINVAL, "record size does not match kp_cap");
         if (reinterpret_cast<uintptr_t>(d_records) & 3) throw Error(ORBFE_EINVAL, "records must be 4-byte aligned");
-        for (int l = 0; l < h->geo.nlevels; ++l)  // the compact format's 12-bit level coordinates (k_pack_compact)
-            if (h->geo.lv[l].w > kMaxLevelSide || h->geo.lv[l].h > kMaxLevelSide)
-                throw Error(ORBFE_EINVAL, "compact records hold level coordinates below 4096 px only");
+        for (int l = 0; l < h->geo.nlevels; ++l)  // the compact format's 14-bit level coordinates (k_pack_compact)
+            if (h->geo.lv[l].w > (1 << kCompactXYBits) || h->geo.lv[l].h > (1 << kCompactXYBits))
+                throw Error(ORBFE_EINVAL, "compact records hold level coordinates below 16384 px only");
         hipPointerAttribute_t pa{};
         if (hipPointerGetAttributes(&pa, d_records) != hipSuccess || pa.type != hipMemoryTypeDevice) {
             (void)hipGetLastError();
@@ -1951,8 +1988,8 @@ int orbfe_debug_candidates(orbfe_handle h, int32_t level, int32_t* xyr, int32_t 
             for (int j = 0; j < cnt[i]; ++j, ++n) {
                 if (n >= cap) continue;
                 const uint32_t k = slots[cg.slot_off + j];
-                xyr[3 * n] = (int)(k & 0xFFF) - kBorder;
-                xyr[3 * n + 1] = (int)((k >> 12) & 0xFFF) - kBorder;
+                xyr[3 * n] = (int)((k & 0xFFFFFFu) % (uint32_t)L.w) - kBorder;
+                xyr[3 * n + 1] = (int)((k & 0xFFFFFFu) / (uint32_t)L.w) - kBorder;
                 xyr[3 * n + 2] = (int)(k >> 24);
             }
         }
@@ -1974,8 +2011,8 @@ int orbfe_debug_selected(orbfe_handle h, int32_t level, int32_t* xyr, int32_t ca
         *n_out = n;
         if (n > cap) throw Error(ORBFE_ECAPACITY, "buffer too small");
         for (int i = 0; i < n; ++i) {
-            xyr[3 * i] = (int)(kp[i] & 0xFFF) - kBorder;
-            xyr[3 * i + 1] = (int)((kp[i] >> 12) & 0xFFF) - kBorder;
+            xyr[3 * i] = (int)((kp[i] & 0xFFFFFFu) % (uint32_t)L.w) - kBorder;
+            xyr[3 * i + 1] = (int)((kp[i] & 0xFFFFFFu) / (uint32_t)L.w) - kBorder;
             xyr[3 * i + 2] = (int)(kp[i] >> 24);
         }
     });

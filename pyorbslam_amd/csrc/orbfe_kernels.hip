@@ -125,7 +125,7 @@ __device__ __forceinline__ CellGeo load_cell(const CellGeo* __restrict__ cells, 
     const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
     CellGeo cg;
     cg.level = (int16_t)(w0 & 0xFFFFu);
-    cg.pad = (int16_t)(w0 >> 16);
+    cg.kw = (int16_t)(w0 >> 16);
     cg.x0 = (int16_t)(w1 & 0xFFFFu);
     cg.y0 = (int16_t)(w1 >> 16);
     cg.x1 = (int16_t)(w2 & 0xFFFFu);
@@ -133,6 +133,23 @@ __device__ __forceinline__ CellGeo load_cell(const CellGeo* __restrict__ cells, 
     cg.slot_off = (int)w3;
     cg.slot_cap = (int)w4;
     return cg;
+}
+
+// A packed level key's coordinates ((x + y * w) | score << 24, kKeyXYBits): y = mul_hi(xy, mag) >> sh is
+// floor(xy / w) for every xy < 2^24 (mag = ceil(2^(31 + s) / w), sh = s - 1, s = ceil(log2 w): the error term
+// xy * (mag * w - 2^(31 + s)) < 2^24 * w < 2^(31 + s)), then x = xy - y * w (both < 2^24: v_mad_u32_u24).
+struct KeyDiv {
+    uint32_t w, mag, sh;
+};
+__device__ __forceinline__ KeyDiv key_div(const LevelGeo& L) {
+    return KeyDiv{(uint32_t)__builtin_amdgcn_readfirstlane(L.w), (uint32_t)__builtin_amdgcn_readfirstlane((int)L.kmag),
+                  (uint32_t)__builtin_amdgcn_readfirstlane(L.ksh)};
+}
+__device__ __forceinline__ void key_xy(uint32_t k, KeyDiv kd, int& x, int& y) {
+    const uint32_t xy = k & 0xFFFFFFu;
+    const uint32_t q = __umulhi(xy, kd.mag) >> kd.sh;
+    y = (int)q;
+    x = (int)(xy - __umul24(q, kd.w));
 }
 
 // XCD-aware remap of a (gridDim.x, gridDim.y) grid.  Hardware block i (flattened, x fastest) runs on
@@ -1078,7 +1095,8 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
                 const int na = max(imax3(t_0, m_0, b_0), imax3(c1, c2, ownb));
                 const int nb = max(imax3(t_3, m_3, b_3), imax3(c1, c2, owna));
                 // (x + 3, y + 3) = (e % RP + 1, e / RP + 3)
-                const uint32_t xy = (uint32_t)(cg.x0 + (int)((uint32_t)e % RP) + 1) | ((uint32_t)(cg.y0 + (int)((uint32_t)e / RP) + 3) << 12);
+                const uint32_t xy = (uint32_t)(cg.x0 + (int)((uint32_t)e % RP) + 1) +
+                                    __umul24((uint32_t)(cg.y0 + (int)((uint32_t)e / RP) + 3), (uint32_t)cg.kw);
                 const uint32_t reca = xy | ((uint32_t)(owna - 1) << 24);
                 const uint32_t recb = (xy + 1u) | ((uint32_t)(ownb - 1) << 24);
                 auto keep = [&](int th, uint64_t& ba, uint64_t& bb, int& t, uint32_t* dst) {
@@ -1171,8 +1189,11 @@ struct OctLds {
     uint16_t* kn;
 };
 
-__device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
-    const int x = (int)(key & 0xFFFu) - kBorder, y = (int)((key >> 12) & 0xFFFu) - kBorder;
+__device__ __forceinline__ int quad_of(uint32_t key, uint64_t box, KeyDiv kv) {
+    int x, y;
+    key_xy(key, kv, x, y);
+    x -= kBorder;
+    y -= kBorder;
     const int x0 = (int16_t)(box & 0xFFFF), y0 = (int16_t)((box >> 16) & 0xFFFF);
     const int x1 = (int16_t)((box >> 32) & 0xFFFF), y1 = (int16_t)((box >> 48) & 0xFFFF);
     const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);  // ceil((float)d/2), d >= 0
@@ -1184,13 +1205,13 @@ __device__ __forceinline__ int quad_of(uint32_t key, uint64_t box) {
 // their LDS loads in flight together, and adds a run length to the LDS counter whenever the bin changes.
 template <typename Div>
 __device__ __forceinline__ void octree_count_runs(int K, int t, const uint16_t* kn, const uint32_t* kd, Div div,
-                                                  const uint64_t* box, int* bins) {
+                                                  const uint64_t* box, int* bins, KeyDiv kv) {
     const int per = (K + kOctThreads - 1) / kOctThreads;
     const int kb = min(t * per, K), ke = min(kb + per, K);
     int cur = -1, run = 0;
     auto add = [&](int p, uint32_t key) {
         if (!div(p)) return;
-        const int b = 4 * p + quad_of(key, box[p]);
+        const int b = 4 * p + quad_of(key, box[p], kv);
         if (b != cur) {
             if (run) atomicAdd(&bins[cur], run);
             cur = b;
@@ -1250,6 +1271,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
     };
     mark(0);
     const LevelGeo& L = g.lv[l];
+    const KeyDiv kv = key_div(L);
     const int NC = g.max_ncap;
     int pow2 = 1;
     while (pow2 < NC) pow2 <<= 1;
@@ -1358,7 +1380,9 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
             const int kb = min(t * per, K), ke = min(kb + per, K);
             int cur = -1, run = 0;
             for (int k = kb; k < ke; ++k) {
-                const int x = (int)(kd[k] & 0xFFFu) - kBorder;
+                int x, y;
+                key_xy(kd[k], kv, x, y);
+                x -= kBorder;
                 const int col = min((int)((float)x / L.hx), nIni - 1);
                 kn[k] = (uint16_t)col;
                 if (col != cur) {
@@ -1418,7 +1442,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                 // each thread counts a contiguous run of candidates: consecutive candidates (cell order)
                 // mostly fall into the same child, so a thread adds one run length per change of bin instead
                 // of one LDS atomic per candidate on a handful of hot counters
-                octree_count_runs(K, t, kn, kd, [&](int p) { return cnt[p] > 1; }, box, d.cnt4);
+                octree_count_runs(K, t, kn, kd, [&](int p) { return cnt[p] > 1; }, box, d.cnt4, kv);
                 __syncthreads();
                 mark(9 + 4 * iter);
                 for (int p = t; p < S; p += kOctThreads) {
@@ -1471,7 +1495,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                         const int k = k0 + u * kOctThreads;
                         if (k < K) {
                             const int p = kn[k];
-                            np[u] = cnt[p] > 1 ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p];
+                            np[u] = cnt[p] > 1 ? d.cpos[4 * p + quad_of(kd[k], box[p], kv)] : d.cpos[4 * p];
                         }
                     }
 #pragma unroll
@@ -1495,7 +1519,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                 for (int p = t; p < S; p += kOctThreads) d.proc[p] = 0;
                 if (t == 0) s_P = 0x7fffffff;
                 __syncthreads();
-                octree_count_runs(K, t, kn, kd, [&](int p) { return p < C && cnt[p] > 1; }, box, d.cnt4);
+                octree_count_runs(K, t, kn, kd, [&](int p) { return p < C && cnt[p] > 1; }, box, d.cnt4, kv);
                 for (int p = t; p < C; p += kOctThreads) d.sa[p] = cnt[p] > 1;
                 __syncthreads();
                 const int M = block_excl_scan(d.sa, C, scan_tmp);
@@ -1583,7 +1607,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(Geo g, const CellGeo* __
                         const int k = k0 + u * kOctThreads;
                         if (k < K) {
                             const int p = kn[k];
-                            np[u] = d.proc[p] ? d.cpos[4 * p + quad_of(kd[k], box[p])] : d.cpos[4 * p];
+                            np[u] = d.proc[p] ? d.cpos[4 * p + quad_of(kd[k], box[p], kv)] : d.cpos[4 * p];
                         }
                     }
 #pragma unroll
@@ -1865,6 +1889,7 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     };
     mark(0);
     const LevelGeo& L = g.lv[l];
+    const KeyDiv kv = key_div(L);
     const int NC = g.max_ncap;
     ObLds d;
     ob_carve(NC, g.oct_bins_max, maxcell, g.oct_tab_max, g.oct_kblk_max, [&](int id, size_t off) {
@@ -1948,8 +1973,10 @@ __global__ __launch_bounds__(NT) void k_octree_bins(Geo g, const CellGeo* __rest
     const uint32_t* X = d.tab;
     const uint32_t* Y = d.tab + nx;
     auto key_code = [&](uint32_t v) {
-        const int x = min(max((int)(v & 0xFFFu) - kBorder, 0), nx - 1);
-        const int y = min(max((int)((v >> 12) & 0xFFFu) - kBorder, 0), ny - 1);
+        int x, y;
+        key_xy(v, kv, x, y);
+        x = min(max(x - kBorder, 0), nx - 1);
+        y = min(max(y - kBorder, 0), ny - 1);
         return X[x] | Y[y];
     };
     // The first sweep, every key once: keys k = t, t + NT, ... (consecutive keys in consecutive lanes:
@@ -3123,6 +3150,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // the level's size in SGPRs for the whole wave (a per-keypoint s_load of the kernel argument would come
     // with an s_waitcnt lgkmcnt(0) that also drains the wave's LDS traffic)
     const int Lw = __builtin_amdgcn_readfirstlane(L.w), Lh = __builtin_amdgcn_readfirstlane(L.h);
+    const KeyDiv kv = key_div(L);
     const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(lvl, (uint32_t)(stride * Lh), &bias);
     uint32_t* src = s_src[wid];
     uint32_t* hb = s_h[wid];
@@ -3200,8 +3228,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     int cx = 0, cy = 0;
     if (nk > 0) {
         const uint32_t k = key_of(0);
-        cx = (int)(k & 0xFFF);
-        cy = (int)((k >> 12) & 0xFFF);
+        key_xy(k, kv, cx, cy);
         if (inside(cx)) issue(cx, cy);
     }
     auto w4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | (b << 8) | (c << 16) | (d << 24); };
@@ -3220,8 +3247,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     };
     auto prefetch = [&](int jn) {  // the loads of keypoint jn's window in flight from here
         const uint32_t k = key_of(jn);
-        cx = (int)(k & 0xFFF);
-        cy = (int)((k >> 12) & 0xFFF);
+        key_xy(k, kv, cx, cy);
         if (inside(cx)) issue(cx, cy);
     };
     // ---- horizontal taps of the disc's (row pair, group) items: src -> hb
@@ -3469,7 +3495,7 @@ __device__ __forceinline__ double py_round(double v) { return rint(v); }  // Pyt
 // coordinates k_orb will write (ORBextractor.cpp:1094-1100: x = f32(level x) * scale[l] for l > 0) and the
 // index iR = the level-major position — so the buckets need the octree only, and the frame and batch paths
 // build them inside k_orb's launch (extra workgroups, stereo_bucket_pair) instead of after it.
-// cnt: H + 1 ints of LDS, tmp: 257 + 2 kMaxLevels + 1 ints.
+// cnt: H + 1 ints of LDS, tmp: 257 + 5 kMaxLevels + 1 ints.
 template <int NT>
 __device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, int* cnt, int* tmp) {
     const int t = threadIdx.x;
@@ -3482,7 +3508,13 @@ __device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, in
     int* scan_tmp = tmp;
     float* s_scale = (float*)(tmp + 257);     // per-octave scales (a lane-indexed kernel-argument read would be
     int* s_pre = tmp + 257 + kMaxLevels;     // a vector memory load); first right keypoint of every level
-    if (t < kMaxLevels) s_scale[t] = g.scale[t];
+    uint32_t* s_kd = (uint32_t*)(tmp + 257 + 2 * kMaxLevels + 1);  // every level's key divisor (w, mag, sh)
+    if (t < kMaxLevels) {
+        s_scale[t] = g.scale[t];
+        s_kd[3 * t] = (uint32_t)g.lv[t].w;
+        s_kd[3 * t + 1] = g.lv[t].kmag;
+        s_kd[3 * t + 2] = (uint32_t)g.lv[t].ksh;
+    }
     if (t == 0) {
         int p0 = 0;
         for (int l = 0; l < kMaxLevels; ++l) {
@@ -3500,7 +3532,9 @@ __device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, in
 #pragma unroll
         for (int j = 1; j < kMaxLevels; ++j) l += j < g.nlevels && s_pre[j] <= i;
         const uint32_t key = lk[g.lv[l].kp_off + (i - s_pre[l])];
-        const float xl = (float)(int)(key & 0xFFFu), yl = (float)(int)((key >> 12) & 0xFFFu);
+        int xi, yi;
+        key_xy(key, KeyDiv{s_kd[3 * l], s_kd[3 * l + 1], s_kd[3 * l + 2]}, xi, yi);
+        const float xl = (float)xi, yl = (float)yi;
         x = l ? __fmul_rn(xl, s_scale[l]) : xl;
         y = l ? __fmul_rn(yl, s_scale[l]) : yl;
     };
@@ -3537,7 +3571,7 @@ __device__ void stereo_bucket_pair(const Geo& g, const StereoArgs& A, int pr, in
 template <int NT>
 __global__ __launch_bounds__(NT) void k_stereo_bucket(Geo g, StereoArgs A) {
     extern __shared__ __attribute__((aligned(16))) int cnt[];  // H + 1 counters
-    __shared__ int tmp[257 + 2 * kMaxLevels + 1];
+    __shared__ int tmp[257 + 5 * kMaxLevels + 1];
     stereo_bucket_pair<NT>(g, A, blockIdx.x, cnt, tmp);
 }
 
@@ -4197,13 +4231,13 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a, uint8_t* __restrict__ 
 }
 
 // Compact records (orbfe_batch_pack_compact_device, pyorbslam_amd/dist.py unpack_compact): counts L, R (2 x i32)
-// | keypoints L, R (cap x {u32 x | y << 12 | octave << 24 in level pixels, f32 angle}) | descriptors L, R
+// | keypoints L, R (cap x {u32 x | y << 14 | octave << 28 in level pixels, f32 angle}) | descriptors L, R
 // (cap x 32 B) | u_right, depth (cap x f32) | scores L, R (cap x u8) | status (cap x i8): 8 + 91 cap bytes
 // against 8 + 121 cap.  A keypoint's x, y, size and response follow from (x, y, octave, score) on the host
 // exactly as k_orb computed them (x = f32(level x) * scale[octave]; the level coordinate is recovered here
-// as rint(x * inv_scale), exact for coordinates < 2^22).  The record keeps 12 bits per level coordinate and 8
-// bits of response: exact only while every level is at most 4 095 px per side (build_geometry's limit,
-// kMaxLevelSide; orbfe_batch_pack_compact_device re-checks it) and the FAST score M - 1 <= 254 (u8 pixels).
+// as rint(x * inv_scale), exact for coordinates < 2^22).  The record keeps 14 bits per level coordinate
+// (kCompactXYBits) and 8 bits of response: exact while every level is at most 16 383 px per side
+// (orbfe_batch_pack_compact_device refuses larger geometries) and the FAST score M - 1 <= 254 (u8 pixels).
 __global__ __launch_bounds__(256) void k_pack_compact(PackArgs a, CompactScales sc, uint8_t* __restrict__ out, int pair0) {
     const int p = blockIdx.y, gp = pair0 + p, t = blockIdx.x * 256 + threadIdx.x, nt = gridDim.x * 256;
     uint8_t* rec = out + (int64_t)p * a.rec_bytes;
@@ -4217,9 +4251,10 @@ __global__ __launch_bounds__(256) void k_pack_compact(PackArgs a, CompactScales 
         for (int64_t i = t; i < cap; i += nt) {
             const orbfe_keypoint k = kp[i];
             const int o = k.octave & 15;
-            const uint32_t x = (uint32_t)__float2int_rn(k.x * sc.inv_scale[o]) & 0xFFFu;
-            const uint32_t y = (uint32_t)__float2int_rn(k.y * sc.inv_scale[o]) & 0xFFFu;
-            kw[2 * i] = x | (y << 12) | ((uint32_t)o << 24);
+            const uint32_t m = (1u << kCompactXYBits) - 1u;
+            const uint32_t x = (uint32_t)__float2int_rn(k.x * sc.inv_scale[o]) & m;
+            const uint32_t y = (uint32_t)__float2int_rn(k.y * sc.inv_scale[o]) & m;
+            kw[2 * i] = x | (y << kCompactXYBits) | ((uint32_t)o << (2 * kCompactXYBits));
             kw[2 * i + 1] = __float_as_uint(k.angle);
             sb[i] = (uint8_t)(int)k.response;
         }

@@ -93,10 +93,10 @@ def unpack_compact(kp_cap: int, rec: np.ndarray, scales) -> dict:
     for s, (name, n) in enumerate((("kps_left", nl), ("kps_right", nr))):
         kw = rec[o_kp + 8 * kp_cap * s:o_kp + 8 * kp_cap * s + 8 * n].view(np.uint32).reshape(n, 2)
         xyo = kw[:, 0]
-        oct_ = (xyo >> 24).astype(np.int32)
+        oct_ = (xyo >> 28).astype(np.int32)  # x | y << 14 | octave << 28 (kCompactXYBits)
         k = np.empty(n, KP_DTYPE)
-        k["x"] = (xyo & 0xFFF).astype(np.float32) * sc[oct_]
-        k["y"] = ((xyo >> 12) & 0xFFF).astype(np.float32) * sc[oct_]
+        k["x"] = (xyo & 0x3FFF).astype(np.float32) * sc[oct_]
+        k["y"] = ((xyo >> 14) & 0x3FFF).astype(np.float32) * sc[oct_]
         k["size"] = size[oct_]
         k["angle"] = kw[:, 1].view(np.float32)
         o_sc = 8 + 88 * kp_cap + s * kp_cap

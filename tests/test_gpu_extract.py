@@ -244,3 +244,109 @@ def test_reference_refused_geometries_gpu():
             ORBextractor(**prm).extract(img)
         with pytest.raises(ValueError):
             O.OracleExtractor(**prm).extract(img)
+
+
+# level sides above 4 095 px.  The packed level keys hold a pixel's row-major index in 24
+# bits (orbfe_common.h kKeyXYBits), so every level of at most 2^24 pixels is accepted, whatever its aspect.
+BIG = [(600, 4500), (2300, 4500), (4500, 2500)]  # (h, w): wide-short, wide, tall (level 0 above 4 095 px)
+
+
+@pytest.mark.parametrize("hw", BIG)
+def test_level_sides_above_4095_px_bit_exact(hw):
+    """One extraction of a 4 500 px wide (or high) image — the cascade pyramid, FAST cells, the octree over
+    a level of more than 4 096 columns (or rows), k_orb — and its sheared pyramid, against the oracle."""
+    h, w = hw
+    img = synth.make_pair(410 + w % 7, w, h)[0]
+    ex = ORBextractor(**KITTI)
+    kps, desc = ex.extract(img)
+    oe = O.OracleExtractor(**KITTI)
+    okps, odesc = oe.extract(img)
+    assert len(kps) > 1000
+    i, a, b = _first_diff(kps, okps)
+    assert i == len(kps) == len(okps), f"{hw}: keypoint {i} differs: {a} vs {b}"
+    assert np.array_equal(desc, odesc)
+    k0 = kps[kps["octave"] == 0]
+    assert max(k0["x"].max(), k0["y"].max()) > 4095
+    got, want = ex.GetImagePyramid(), oe.sheared_pyramid()
+    for l, (p, q) in enumerate(zip(got, want)):
+        assert p.shape == q.shape and np.array_equal(p, q), f"{hw} level {l}"
+
+
+def test_level_sides_above_4095_px_frame_and_batch():
+    """The 4 500 x 600 geometry through the per-frame stereo path (both extractions, the row buckets fused in
+    k_orb, k_stereo, the lazy sheared views) and through a 16-pair batch (32 images: the per-level k_resize_rows
+    launches with their chunk loop, the 4-cell k_detect waves, 256-thread octree workgroups, the compact
+    records), pairs checked bit for bit against the oracle and the stereo restatement."""
+    import torch
+    from oracle import stereo_oracle
+    from pyorbslam_amd import dist as D
+    from pyorbslam_amd.batch import StereoFrontEnd
+    from pyorbslam_amd.frame import to_reference_lists
+    from conftest import BF, FX
+    h, w = 600, 4500
+    pairs = [synth.make_pair(430 + i, w, h) for i in range(16)]
+
+    def oracle_pair(L, R):
+        oL, oR = O.OracleExtractor(**KITTI), O.OracleExtractor(**KITTI)
+        kl, dl = oL.extract(L)
+        kr, dr = oR.extract(R)
+        t = oL.tables()
+        ou, od, _ = stereo_oracle.compute_stereo_matches(kl, kr, dl, dr, oL.sheared_pyramid(), oR.sheared_pyramid(),
+                                                         t["scale"], t["inv_scale"], BF, np.float32(FX))
+        return kl, dl, kr, dr, ou, od, oL.sheared_pyramid(), oR.sheared_pyramid()
+
+    def same_lists(a, b):
+        sa, va = stereo_oracle.encode(a)
+        sb, vb = stereo_oracle.encode(b)
+        return np.array_equal(sa, sb) and np.array_equal(va, vb)
+
+    # per-frame path
+    left, right = ORBextractor(**KITTI), ORBextractor(**KITTI)
+    L, R = pairs[0]
+    gk, gd, hk, hd = left.operator_kd_stereo(L, R, right, BF, np.float32(FX))
+    kl, dl, kr, dr, ou, od, pl, pr = oracle_pair(L, R)
+    assert gk.tobytes() == kl.tobytes() and np.array_equal(gd, dl)
+    assert hk.tobytes() == kr.tobytes() and np.array_equal(hd, dr)
+    u, d = to_reference_lists(left.stereo_result, gk, BF)
+    assert same_lists(u, ou) and same_lists(d, od)
+    assert sum(s == 1 for s in left.stereo_result["status"]) > 100
+    for a, b in zip(list(left.GetImagePyramid()) + list(right.GetImagePyramid()), list(pl) + list(pr)):
+        assert np.array_equal(a, b)
+    # batch path, 16 pairs in one enqueue
+    fe = StereoFrontEnd(w, h, max_pairs=16, lanes=1)
+    imgs = torch.from_numpy(np.stack([x for p in pairs for x in p])).cuda()
+    fe.enqueue(imgs, 16, BF, np.float32(FX), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert fe.overflow() == 0
+    for p in (5, 15):
+        kl, dl, kr, dr, ou, od, _, _ = oracle_pair(*pairs[p])
+        k, dd = fe.fetch_image(2 * p)
+        k2, dd2 = fe.fetch_image(2 * p + 1)
+        assert k.tobytes() == kl.tobytes() and np.array_equal(dd, dl), f"pair {p} left"
+        assert k2.tobytes() == kr.tobytes() and np.array_equal(dd2, dr), f"pair {p} right"
+        u, d = to_reference_lists(fe.fetch_stereo(p), k, BF)
+        assert same_lists(u, ou) and same_lists(d, od), f"pair {p} stereo"
+    # compact records (14-bit level coordinates) rebuild the 4 500 px keypoints exactly
+    buf = torch.zeros((16, D.compact_record_bytes(fe.kp_cap)), dtype=torch.uint8, device="cuda")
+    D.pack_device([fe], [16], buf, compact=True)
+    torch.cuda.synchronize()
+    rec = D.unpack_compact(fe.kp_cap, buf[15].cpu().numpy(), fe.scales)
+    k, _ = fe.fetch_image(30)
+    assert rec["kps_left"].tobytes() == k.tobytes() and (k["x"] > 4095).any()
+
+
+def test_levels_above_2_pow_24_pixels_refused():
+    """The documented limit: a level of more than 2^24 pixels does not fit the packed keys
+    and is refused with ORBFE_EINVAL naming the limit (the reference accepts it); a 600 x 4 500 image (tall,
+    aspect below 0.5) is refused as the reference's DistributeOctTree indexes out of range on it
+    (nIni = round(spanX / spanY) = 0, ORBextractor.cpp:543-568), ValueError like the oracle's refusal."""
+    from pyorbslam_amd._lib import OrbfeError
+    img = np.zeros((4200, 4200), np.uint8)
+    img[::7, ::5] = 200
+    with pytest.raises(OrbfeError, match="2\\^24"):
+        ORBextractor(**KITTI).extract(img)
+    tall = synth.make_pair(5, 600, 4500)[0]
+    with pytest.raises(ValueError, match="DistributeOctTree"):
+        ORBextractor(**KITTI).extract(tall)
+    with pytest.raises(ValueError):
+        O.OracleExtractor(**KITTI).extract(tall)
