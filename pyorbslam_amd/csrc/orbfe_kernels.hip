@@ -3592,33 +3592,46 @@ __device__ __forceinline__ uint32_t row16_min(uint32_t v) {
     return v;
 }
 
-// n <= 24 consecutive pixels (row r, columns c0 ..) of the sheared view of a level as 6 dwords (byte j of the run = byte j % 4 of w[j / 4]).
+// n consecutive pixels (row r, columns c0 ..) of the sheared view of a level as NDW dwords (byte j of the run =
+// byte j % 4 of w[j / 4]; n + 3 <= 4 NDW: the left patch's 11 bytes in 4 dwords, the right strip's 21 in 6).
+// The interior path loads them as one dwordx4 (+ one dwordx2): 2 memory instructions per row instead of 6 dword
+// loads (partially out-of-range dwords read 0 per dword, the loads are not merged past it).
 // rs: a wave-uniform resource over the buffer holding the level (the pair's input image or its workspace),
 // bias its base misalignment, lvl_off the level's byte offset in it (per lane): the loads need no
 // per-lane resource (a per-lane one makes the compiler waterfall every load over the wave's distinct
 // resources).  Bytes of the 24 past the run are whatever follows it in the buffer (0 past its end);
 // k_stereo masks them.  lvl: the level itself, for the reflect-101 path at its border.
+template <int NDW>
 __device__ __forceinline__ void sheared_words(__amdgpu_buffer_rsrc_t rs, uint32_t bias, uint32_t lvl_off,
                                               const uint8_t* lvl, int stride, int w, int h, int r, int c0, int n,
-                                              uint32_t (&wd)[6]) {
+                                              uint32_t (&wd)[NDW]) {
+    static_assert(NDW == 4 || NDW == 6, "4 or 6 dwords");
     const int pw = w + 2 * kEdge;
     const int f = kEdge * pw + kEdge + r * w + c0;
     int pr = f / pw, pc = f - pr * pw;
     if (pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w) {
         const uint32_t off = bias + lvl_off + (uint32_t)((pr - kEdge) * stride + (pc - kEdge));
         const uint32_t sh = off & 3u, al = off - sh;
-        uint32_t d[7];
+        uint32_t d[NDW + 1];
+        const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, al, 0, 0));
+        d[0] = q.x;
+        d[1] = q.y;
+        d[2] = q.z;
+        d[3] = q.w;
+        if constexpr (NDW == 6) {
+            const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al + 16u, 0, 0));
+            d[4] = t.x;
+            d[5] = t.y;
+        }
+        d[NDW] = 0;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4u * k, 0, 0);
-        d[6] = 0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) wd[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        for (int k = 0; k < NDW; ++k) wd[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
         return;
     }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) wd[k] = 0;
+    for (int k = 0; k < NDW; ++k) wd[k] = 0;
 #pragma unroll
-    for (int j = 0; j < 21; ++j) {
+    for (int j = 0; j < 4 * NDW - 3; ++j) {
         if (j < n) wd[j >> 2] |= (uint32_t)lvl[(int64_t)reflect101(pr - kEdge, h) * stride + reflect101(pc - kEdge, w)]
                                  << (8 * (j & 3));
         if (++pc == pw) {
@@ -3690,7 +3703,12 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         // descriptors (read whether or not the gates pass) are in flight together — two dependent round
         // trips per step instead of two per candidate
         constexpr int kStU = 2;
+#ifdef ORBFE_X_ST_NOSEARCH  // ablation (wrong results): no candidate loop, every keypoint matches right keypoint 0
+        key = 0u;
+        for (int k0 = e; k0 < e; k0 += 16 * kStU) {
+#else
         for (int k0 = b + sl; k0 < e; k0 += 16 * kStU) {
+#endif
             int iR[kStU];
 #pragma unroll
             for (int j = 0; j < kStU; ++j) iR[j] = k0 + 16 * j < e ? (int)bidxs[k0 + 16 * j] : -1;
@@ -3745,8 +3763,11 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         // iniu < 0 or endu >= cols (:240-243); the slices stay inside the level otherwise
         do_sad = !(scaleduR0 < 0 || scaleduR0 + 11 >= lw) && scaledvL - 5 >= 0 && scaledvL + 6 <= lh &&
                  scaleduL - 5 >= 0 && scaleduL + 6 <= lw && scaleduR0 - 10 >= 0;
+#ifdef ORBFE_X_ST_NOSAD  // ablation (wrong results): no window staging, SAD or parabola
+        do_sad = false;
+#endif
         if (do_sad && sl < 11) {  // lane sl stages window row sl
-            uint32_t wl[6], wr[6];
+            uint32_t wl[4], wr[6];
             if (oct == 0) {
                 sheared_words(rsL0, bL0, 0u, lvlL, lstride, lw, lh, scaledvL - 5 + sl, scaleduL - 5, 11, wl);
                 sheared_words(rsR0, bR0, 0u, lvlR, lstride, lw, lh, scaledvL - 5 + sl, scaleduR0 - 10, 21, wr);

@@ -8,6 +8,8 @@ name=$1
 defs=$2
 root=$(cd "$(dirname "$0")/../.." && pwd)
 out=$root/pyorbslam_amd/_lib/variants/$name
+# AB=1: into _ab/NAME instead (travels with gpurun; tools/dbg/ab.sh)
+[ "${AB:-0}" = 1 ] && out=$root/_ab/$name
 tmp=$(mktemp -d)
 cp -r "$root/pyorbslam_amd" "$root/include" "$root/Makefile" "$tmp/"
 rm -rf "$tmp/pyorbslam_amd/_lib"
