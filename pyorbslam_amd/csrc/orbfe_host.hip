@@ -1954,6 +1954,12 @@ int orbfe_microbench(orbfe_handle h, int32_t stage, int32_t variant, int32_t rep
                     if (h->last_pairs <= 0) throw Error(ORBFE_ESTATE, "no stereo batch");
                     enqueue_stereo_batch(*h, h->last_pairs, h->last_bf, h->last_fx, s);
                     break;
+                case 5:
+                    // the HBM writes a blurred pyramid would add (every level of every image, w x h bytes each):
+                    // the lower bound of its cost in any design that writes one
+                    h->d_shear.ensure((size_t)n * (size_t)g.shear_bytes);
+                    HIPCK(hipMemsetD8Async((hipDeviceptr_t)h->d_shear.p, 0x5A, (size_t)n * (size_t)g.shear_bytes, s));
+                    break;
                 default:
                     throw Error(ORBFE_EINVAL, "bad stage");
             }

@@ -3329,6 +3329,12 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 uint32_t addr;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(addr) : "v"(xb >> 1), "s"(0xA0u), "v"((yb << 2) + kc));
                 lds_u32* p = (lds_u32*)(uintptr_t)addr;
+#ifdef ORBFE_X_ORB_PREBLURRED
+                // ablation (wrong bits; VERDICT r5 item 6's bound): a sample read as ONE byte of a window that
+                // would already be blurred (a blurred pyramid level) instead of the 7 vertical taps
+                v2[e] = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)addr;
+                continue;
+#endif
                 const uint32_t p0 = p[0], p1 = p[kHDw], p2 = p[2 * kHDw], p3 = p[3 * kHDw];
                 const uint32_t sh = xb << 4;
                 uint32_t s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_alignbit(p1, p0, sh)), w2(18, 34), 32768u, false);
@@ -3363,7 +3369,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         stage();
         const int ax = cx, ay = cy;
         if (has_b) prefetch(j + 1);
+#ifndef ORBFE_X_ORB_PREBLURRED  // (the ablation: no horizontal pass either)
         hpass();
+#endif
         int m10a, m01a, m10b = 0, m01b = 0;
         centroid(m10a, m01a);
         int bx = 0, by = 0;
@@ -3393,7 +3401,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         record(j, ax, ay, angA, keyA);
         if (has_b) {
             wave_sync_lds();  // BRIEF A's hb reads are complete (waited before its ballots)
+#ifndef ORBFE_X_ORB_PREBLURRED
             hpass();
+#endif
             wave_sync_lds();  // hb complete
             brief(aB, bB, j + 1);
             record(j + 1, bx, by, angB, keyB);

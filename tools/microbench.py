@@ -33,7 +33,7 @@ def main():
             res[it].append(round(ms.value * 1000, 1))
             fe.enqueue(imgs)  # restore real stage outputs for the next item
             torch.cuda.synchronize()
-    names = ["resize", "detect", "octree", "describe", "stereo"]
+    names = ["resize", "detect", "octree", "describe", "stereo", "blurwrite"]
     for it, v in res.items():
         st, var = map(int, it.split(":"))
         print(f"{names[st]:9s} v{var}: us per launch {v}  (min {min(v)})")
