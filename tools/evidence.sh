@@ -34,6 +34,8 @@ timeout -k 10 120 python bench.py --gpus 2 > "$out/bench_gpus2_refuses.log" 2>&1
 echo "== bench_gpus2_refuses rc=$rc (expected 2)"; tail -n 2 "$out/bench_gpus2_refuses.log"
 [ $rc -eq 2 ] || exit 1
 step bench_gpus2_gloo 300 env ORBFE_DIST_BACKEND=gloo python bench.py --gpus 2 --pairs 64 --steps 5 --warmup 2 --no-parity --roofline-steps 0
+step bench_c4_gloo8 300 env ORBFE_DIST_BACKEND=gloo OMP_NUM_THREADS=2 python bench.py --gpus 8 --total-pairs 64 --pairs 8 --steps 3 --warmup 1 --cpu-sample 0 --no-c3 --no-host-fed --roofline-steps 1
+step rccl_single 150 python tools/rccl_probe.py --single
 step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/ktrace" -o run -- python bench.py --cpu-sample 0 --no-c4 --no-host-fed --no-c3 --no-c5
 step ktrace_share8 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_share8" -o run -- python tools/small_trace.py --pairs 8 --steps 50
 step ktrace_frame 120 rocprofv3 --kernel-trace --output-format csv -d "$out/ktrace_frame" -o run -- python tools/small_trace.py --frame --steps 50
