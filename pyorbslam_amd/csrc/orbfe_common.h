@@ -54,6 +54,8 @@ struct LevelGeo {
     // k_resize of this level: groups per row (multiple of 4), most source rows per band, source stride;
     // the launch's dynamic LDS is sized from these (the small levels fit more workgroups per CU)
     int rs_ngrp, rs_nsrc, rs_sp;
+    int rs_rows;         // k_resize_rows output rows per band: kRsRows, fewer for a level whose source rows per band
+                         // would not fit the LDS (levels wider than ~7 000 px)
     int64_t shear_off;   // byte offset of the level's w x h sheared view inside an image's k_shear output
     // k_octree (bins): every candidate's quadtree path as a Morton code, code = X[x_rel] | Y[y_rel]
     // (host tables at oct_xt / oct_yt of the octree table buffer): column in the bits above 2 * oct_d,

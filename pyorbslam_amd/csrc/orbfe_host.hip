@@ -561,19 +561,24 @@ void build_geometry(orbfe_ctx& c, int W, int H) {
     g.rs_ngrp = 4;
     for (int l = 1; l < L; ++l) {
         LevelGeo& Lg = g.lv[l];
-        Lg.rs_nsrc = 1;
-        for (int dy0 = 0; dy0 < Lg.h; dy0 += kRsRows) {
-            const int dy1 = std::min(dy0 + kRsRows, Lg.h);
-            Lg.rs_nsrc = std::max(Lg.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
-        }
         Lg.rs_sp = l >= 2 ? g.lv[l - 1].pitch : g.W;
+        // the band's source rows are staged whole (k_resize_rows' dynamic LDS: nsrc x sp bytes): a level so wide
+        // that 16-row bands would not fit takes 8-, 4-, 2- or 1-row bands (round 6; 16 up to ~7 000 px)
+        for (Lg.rs_rows = kRsRows;; Lg.rs_rows /= 2) {
+            Lg.rs_nsrc = 1;
+            for (int dy0 = 0; dy0 < Lg.h; dy0 += Lg.rs_rows) {
+                const int dy1 = std::min(dy0 + Lg.rs_rows, Lg.h);
+                Lg.rs_nsrc = std::max(Lg.rs_nsrc, c.yt[Lg.ytab_off + dy1 - 1].sy1 - c.yt[Lg.ytab_off + dy0].sy0 + 1);
+            }
+            if ((int64_t)Lg.rs_nsrc * Lg.rs_sp + 16 <= 150 * 1024 || Lg.rs_rows == 1) break;
+        }
+        if ((int64_t)Lg.rs_nsrc * Lg.rs_sp + 16 > 150 * 1024)
+            throw Error(ORBFE_EINVAL, "image too wide for the k_resize band staging (LDS)");
         Lg.rs_ngrp = ((Lg.w + 3) / 4 + 3) & ~3;
         g.rs_nsrc = std::max(g.rs_nsrc, Lg.rs_nsrc);
         g.rs_sp = std::max(g.rs_sp, Lg.rs_sp);
         g.rs_ngrp = std::max(g.rs_ngrp, Lg.rs_ngrp);
     }
-    if ((int64_t)g.rs_ngrp * 36 + 128 + (int64_t)g.rs_nsrc * g.rs_sp + 16 > 150 * 1024)
-        throw Error(ORBFE_EINVAL, "image too wide for the k_resize band staging (LDS)");
     g.ws_bytes = std::max<int64_t>(ws, 256);
     g.shear_bytes = shear;
     g.slot_total = std::max<int64_t>(slot_off, 1);

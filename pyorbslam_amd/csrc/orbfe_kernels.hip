@@ -379,7 +379,8 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
     xcd_block(bx, img);
     const int t = threadIdx.x, nthr = blockDim.x;
     if (zero_word && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) *zero_word = 0;
-    const int dy0 = bx * kRsRows, nrow = min(kRsRows, L.h - dy0);
+    const int rows = L.rs_rows;  // kRsRows, fewer for very wide levels (LevelGeo::rs_rows)
+    const int dy0 = bx * rows, nrow = min(rows, L.h - dy0);
     const int ngrp = (L.w + 3) >> 2;
     int sstride;
     const uint8_t* src = level_ptr(g, l - 1, in, in_pitch, ws, img, &sstride);
@@ -3945,8 +3946,8 @@ __global__ __launch_bounds__(256) void k_hamming_search(const uint8_t* __restric
 // ------------------------------------------------------------------------------- launchers
 hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitch, uint8_t* ws, const ResizeX* xt,
                          const ResizeY* yt, int n_images, hipStream_t s, int variant, int* zero_word) {
-    dim3 grid((g.lv[l].h + kRsRows - 1) / kRsRows, n_images);
     const LevelGeo& L = g.lv[l];  // LDS sized for this level (tables + its bands' source rows)
+    dim3 grid((L.h + L.rs_rows - 1) / L.rs_rows, n_images);
     // production: k_resize_rows (profiles/r03/resize_rows_ab_r3f.log: 414 -> 394 us per 256 pairs
     // standalone, +0.8 % on the 4-handle step); variants (tools/microbench.py): 4 = the item-mapped
     // k_resize, 1 / 2 = its staging-only / compute-only ablations
@@ -3972,6 +3973,7 @@ hipError_t launch_resize(const Geo& g, int l, const uint8_t* in, int64_t in_pitc
 #ifdef ORBFE_DEV_VARIANTS
     if (L.wide) return hipErrorInvalidValue;  // the round-2 kernel gathers every pixel from the group's 8 bytes
     const size_t lds = (size_t)L.rs_ngrp * 36 + 16 * kRsRows + (size_t)L.rs_nsrc * L.rs_sp + 16;
+    if (L.rs_rows != kRsRows || lds > 150 * 1024) return hipErrorInvalidValue;  // kRsRows-row bands only
     auto k = variant == 1 ? k_resize<1> : variant == 2 ? k_resize<2> : k_resize<0>;  // variant 4: k_resize<0>
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, l, in, in_pitch, ws, xt, yt);
     return hipGetLastError();

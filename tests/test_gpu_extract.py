@@ -248,7 +248,9 @@ def test_reference_refused_geometries_gpu():
 
 # level sides above 4 095 px.  The packed level keys hold a pixel's row-major index in 24
 # bits (orbfe_common.h kKeyXYBits), so every level of at most 2^24 pixels is accepted, whatever its aspect.
-BIG = [(600, 4500), (2300, 4500), (4500, 2500)]  # (h, w): wide-short, wide, tall (level 0 above 4 095 px)
+# (h, w): wide-short, wide, tall (level 0 above 4 095 px); then widths whose resize bands need fewer than 16 rows
+# to fit the LDS (LevelGeo::rs_rows) and whose level-0 octree takes the per-candidate k_octree (bins past 150 KiB)
+BIG = [(600, 4500), (2300, 4500), (4500, 2500), (600, 16000), (1300, 12000)]
 
 
 @pytest.mark.parametrize("hw", BIG)
