@@ -40,3 +40,15 @@ def test_accepted_geometries(wh):
 def test_refused_geometries(wh, needle):
     rc, msg = reserve(*wh)
     assert rc == EINVAL and needle in msg, (rc, msg)
+
+
+def test_parameter_limits():
+    """scale factors above 3.0 (the resize tap windows) and a level needing more than 150 KiB of
+    octree LDS are refused; the reference's own parameters on large images are not."""
+    assert reserve(1241, 376, 3.0, 2)[0] != EINVAL
+    rc, msg = reserve(1241, 376, 3.2, 2)
+    assert rc == EINVAL and "tap windows" in msg
+    rc, msg = reserve(4000, 3000, 3.0, 2)
+    assert rc == EINVAL and "octree LDS" in msg
+    for wh in ((4000, 3000), (3840, 2160), (5000, 3000)):
+        assert reserve(*wh, 1.2, 8, 4000)[0] != EINVAL
