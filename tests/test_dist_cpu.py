@@ -135,3 +135,41 @@ def test_gather_digests_check_every_record_gloo(n_pairs):
     res = q.get()
     assert res[0] is True and res[1] == n_pairs and res[2] == 2 * D.shard(n_pairs, 2, 0)[1] - n_pairs
     assert not any(res[3:])
+
+
+class _FakeFrontEnd:
+    """fetch_image / fetch_stereo of a StereoFrontEnd, from fixed random arrays (no GPU)."""
+
+    def __init__(self, n_pairs, seed, cap=40):
+        rng = np.random.default_rng(seed)
+        self.kp_cap = cap
+        self.pairs = []
+        for p in range(n_pairs):
+            kl, dl, st = _fake(rng, cap, 7 + p)
+            kr, dr, _ = _fake(rng, cap, 3 + p)
+            self.pairs.append((kl, dl, kr, dr, st))
+
+    def fetch_image(self, i):
+        k = self.pairs[i // 2]
+        return (k[0], k[1]) if i % 2 == 0 else (k[2], k[3])
+
+    def fetch_stereo(self, p):
+        return self.pairs[p][4]
+
+
+def test_local_digests_rows_and_padding():
+    """local_digests: one valid row per local pair in handle-major order (what pack_device writes), the digest
+    of the fetched fields; rows past the rank's pairs stay zero.  check_gathered accepts records packed from the
+    same fields and rejects one whose status byte changed."""
+    fes = [_FakeFrontEnd(2, 1), _FakeFrontEnd(1, 2)]
+    dg = D.local_digests(fes, [2, 1], 4)
+    assert dg.shape == (4, D.DIGEST_ROW) and dg[:3, 0].tolist() == [1, 1, 1] and not dg[3].any()
+    recs = np.zeros((4, D.record_bytes(40)), np.uint8)
+    for j, (f, p) in enumerate(((fes[0], 0), (fes[0], 1), (fes[1], 0))):
+        kl, dl, kr, dr, st = f.pairs[p]
+        recs[j] = D.pack(40, kl, dl, kr, dr, st)
+    chk = D.check_gathered(recs, dg, lambda r: D.unpack(40, r))
+    assert chk["ok"] and chk["records_verified"] == 3 and chk["padded_rows_zero"] == 1
+    bad = recs.copy()
+    bad[2, 8 + 2 * 40 * KP_DTYPE.itemsize + 2 * 40 * 32 + 40 * 8] ^= 1  # pair 2's first status byte
+    assert not D.check_gathered(bad, dg, lambda r: D.unpack(40, r))["ok"]
