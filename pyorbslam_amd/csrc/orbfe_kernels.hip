@@ -42,6 +42,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
 }
 
+// Buffer resource over the wave-uniform p, bounded to nbytes bytes.  The halves go through uint32_t: the
+// builtin returns int, and a sign-extended low half OR-ed into the 64-bit address corrupts its high bits
+// whenever bit 31 of the address is set.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bounded_rsrc(const void* p, uint32_t nbytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+}
+
 // Buffer resource over the dword-aligned address at or below the wave-uniform p, bounded to
 // bias + nbytes bytes; *bias = p's misalignment, so byte i of p sits at resource offset bias + i and a
 // dword-aligned load covering it starts at (bias + i) & ~3 (never below the resource base).
@@ -424,20 +435,28 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         }
     };
     chunk(ch);
-    // staging by the first 256 threads (blocks have >= 256): compile-time strides, immediate LDS offsets
+    // staging by the first 256 threads (blocks have >= 256): compile-time strides, immediate LDS offsets.  The
+    // loads go through a wave-uniform buffer resource: one VGPR offset for all slots, the slot and pass in the
+    // SGPR offset, no 64-bit address arithmetic; the range test is one compare of the thread index against a
+    // wave-uniform limit per slot, shared by the load and the LDS store (≈ 8 VALU per staged dword before, a
+    // quarter of the stage's VALU).  The test must guard the load itself: the resource's bounds check does not
+    // include the SGPR offset, so an unguarded slot past the run reads past the buffer.
     if (t < 256) {
+        const __amdgpu_buffer_rsrc_t rsrc = bounded_rsrc((const void*)(uintptr_t)gsrc, (uint32_t)(4 * ndw));
         for (int base = 0; base < ndw; base += 256 * kRsSlots) {
+            const int left = ndw - base;
             uint32_t v[kRsSlots];
 #pragma unroll
             for (int k = 0; k < kRsSlots; ++k) {
-                const int i = base + t + 256 * k;
-                v[k] = i < ndw ? gsrc[i] : 0u;
+                v[k] = 0u;
+                if (t < left - 256 * k)
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (uint32_t)(4 * t), (uint32_t)(4 * (base + 256 * k)), 0);
             }
+            // one LDS address per pass (immediate offsets per slot)
+            lds_w32* sp = s_src + base + t;
 #pragma unroll
-            for (int k = 0; k < kRsSlots; ++k) {
-                const int i = base + t + 256 * k;
-                if (i < ndw) s_src[i] = v[k];
-            }
+            for (int k = 0; k < kRsSlots; ++k)
+                if (t < left - 256 * k) sp[256 * k] = v[k];
         }
     }
     __syncthreads();
@@ -448,11 +467,12 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
         const int dx = 4 * grp;
         const bool tail = dx + 3 >= L.xvec;  // FixedPtCast<int, uchar, 22> past the last SIMD block
         const uint32_t lsrc = src_lds + (uint32_t)sh0 + (uint32_t)sx0;
-        // psy / hp: the previous row's second source row and its taps (full waves walk consecutive rows, and a
-        // row's first source row is mostly the previous row's second: its taps are reused, not recomputed)
+        // psy: the previous row's second source row.  Full waves walk consecutive rows, and a row's first
+        // source row is mostly the previous row's second: its taps are reused, not recomputed.  The two tap
+        // sets alternate between ha and hb over a 2-row unrolled loop, so the reuse needs no register copies
+        // (4-5 v_mov per row and 4-pixel group before)
         int psy = -1;
-        uint32_t hp[4] = {0u, 0u, 0u, 0u};
-        auto row = [&](int rr, bool reuse) {
+        auto row = [&](int rr, uint32_t (&h0)[4], uint32_t (&h1)[4], bool reuse) {
             const ResizeY y = yb[rr];  // full waves: uniform, scalar loads
             const uint32_t r0 = (uint32_t)((y.sy0 - ys_lo) * sstride), r1 = (uint32_t)((y.sy1 - ys_lo) * sstride);
             const uint32_t B0 = (uint32_t)y.b0 << 12, B1 = (uint32_t)y.b1 << 12;
@@ -471,19 +491,10 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
                               : __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(d1, d0, e.w)),
                                                        __builtin_bit_cast(us2, aa.w), 0u, false);
             };
-            uint32_t h0[4], h1[4];
-            if (reuse && y.sy0 == psy) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h0[k] = hp[k];
-            } else {
-                taps(r0, h0);
-            }
+            // h0 holds the taps of source row psy (the previous row's h1) when reuse applies
+            if (!(reuse && y.sy0 == psy)) taps(r0, h0);
             taps(r1, h1);
-            if (reuse) {
-                psy = y.sy1;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) hp[k] = h1[k];
-            }
+            if (reuse) psy = y.sy1;
             uint32_t v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = (__umulhi(h0[k] & ~15u, B0) + __umulhi(h1[k] & ~15u, B1) + 2) >> 2;
@@ -496,12 +507,18 @@ __global__ __launch_bounds__(512) void k_resize_rows(Geo g, int l, const uint8_t
             __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rd, (uint32_t)dx,
                                                   (uint32_t)(rr * L.pitch), 0);
         };
+        uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
         if (!remwave) {  // set s: rows [s * per, (s + 1) * per), consecutive
             const int per = (nrow + nset - 1) / nset, rend = min(set * per + per, nrow);
             psy = -1;
-            for (int rr = set * per; rr < rend; ++rr) row(rr, true);
+            int rr = set * per;
+            for (; rr + 1 < rend; rr += 2) {
+                row(rr, ha, hb, true);
+                row(rr + 1, hb, ha, true);
+            }
+            if (rr < rend) row(rr, ha, hb, true);
         } else {
-            for (int rr = row0; rr < nrow; rr += rstep) row(rr, false);
+            for (int rr = row0; rr < nrow; rr += rstep) row(rr, ha, hb, false);
         }
         if (!MULTI) return;  // one chunk per wave (every level up to 2 048 px): round 3's code exactly
         ch += ch_step;
@@ -3682,7 +3699,6 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     const int nL = A.countL[pr * A.cnt_stride];
     const bool active = iL < nL;
     const orbfe_keypoint* KL = A.kpsL + pr * A.kp_stride;
-    const orbfe_keypoint* KR = A.kpsR + pr * A.kp_stride;
     const uint8_t* DL = A.descL + pr * A.kp_stride * 32;
     const uint8_t* DR = A.descR + pr * A.kp_stride * 32;
     const float2* rinfo = A.rinfo + pr * A.out_stride;
@@ -3698,6 +3714,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
                                  rsRW = aligned_rsrc(wsR, (uint32_t)g.ws_bytes, &bRW);
     if (sl < 11) sad[kq][sl] = 0;
     uint32_t key = 0xFFFFFFFFu;  // (distance << 16) | iR
+    float kx = 0.f;              // x of this lane's best right keypoint (rinfo: the x k_orb writes to KR)
     // the left record is read before the count is known (iL < kp_cap: inside the array), so the two
     // loads overlap
     orbfe_keypoint kl = KL[iL];
@@ -3741,11 +3758,23 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
                 const uint32_t dist = __popc(a0.x ^ b0[j].x) + __popc(a0.y ^ b0[j].y) + __popc(a0.z ^ b0[j].z) +
                                       __popc(a0.w ^ b0[j].w) + __popc(a1.x ^ b1[j].x) + __popc(a1.y ^ b1[j].y) +
                                       __popc(a1.z ^ b1[j].z) + __popc(a1.w ^ b1[j].w);
-                if (ok) key = min(key, (dist << 16) | (uint32_t)iR[j]);
+                if (ok) {
+                    const uint32_t c = (dist << 16) | (uint32_t)iR[j];
+                    if (c < key) {
+                        key = c;
+                        kx = ri[j].x;
+                    }
+                }
             }
         }
     }
+    const uint32_t mine = key;
     key = row16_min(key);
+    // the winner's x from the lane that holds it (keys are unique: a right keypoint is listed once per row
+    // bucket) instead of a KR[bidx] load after the search: one dependent global round trip less per wave
+    const uint64_t holds = __ballot(mine == key);
+    const uint64_t grp_holds = (holds >> (lane & 48)) & 0xFFFFull;
+    const float uR0w = __shfl(kx, grp_holds ? (lane & 48) + __builtin_ctzll(grp_holds) : lane, 64);
     const int best = (int)(key >> 16), bidx = (int)(key & 0xFFFFu);
     int status = 0;
     float uR = -1.f, depth = -1.f;
@@ -3755,7 +3784,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     if (refine) {
         const int oct = kl.octave;
         const double isf = (double)s_isc[oct];
-        const float uR0 = KR[bidx].x;
+        const float uR0 = uR0w;  // == KR[bidx].x
         const int scaleduL = (int)py_round((double)kl.x * isf);
         const int scaledvL = (int)py_round((double)kl.y * isf);
         scaleduR0 = (int)py_round((double)uR0 * isf);
