@@ -884,24 +884,21 @@ __global__ __launch_bounds__(64, (RP == 48 && NS <= 12) ? 5 : 4) void k_detect(G
     constexpr int NS2 = NS / 2;
     const int d = lane & 7, r0 = lane >> 3;
     uint2 raw[NS2];
+    // Every slot loads unconditionally, through a resource bounded to the level (a row past it reads 0): rows
+    // past the ROI and dwords past its width land only in LDS the commit below never writes or in columns
+    // past the ROI, and the per-slot range tests, zero fills and branches are gone (one v_add per slot)
     auto issue = [&](int c) {
         const CellGeo cg = load_cell(cells, c);
         int stride;
         const uint8_t* lvl = level_ptr(g, cg.level, in, in_pitch, ws, img, &stride);
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(lvl);
-        const int rw = cg.x1 - cg.x0, rh = cg.y1 - cg.y0, ndw = (rw + 4) >> 2;  // columns -1 .. rw-1
+        const __amdgpu_buffer_rsrc_t rs = bounded_rsrc(lvl, (uint32_t)(stride * g.lv[cg.level].h));
         const uint32_t lvl_lo = (uint32_t)(uintptr_t)lvl;
         const uint32_t off0 = (uint32_t)((cg.y0 + r0) * stride + cg.x0 - 1);
+        // rows r0 + 8 k share the alignment of row r0 (8 k * stride is a multiple of 4)
+        const uint32_t al0 = off0 - ((lvl_lo + off0) & 3u) + 8u * d;
 #pragma unroll
-        for (int k = 0; k < NS2; ++k) {
-            const int r = r0 + 8 * k;
-            raw[k] = uint2{0u, 0u};
-            if (r < rh && 2 * d <= ndw) {
-                const uint32_t off = off0 + (uint32_t)(8 * k * stride);
-                const uint32_t al = off - ((lvl_lo + off) & 3u);
-                raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al + 8u * d, 0, 0));
-            }
-        }
+        for (int k = 0; k < NS2; ++k)
+            raw[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, al0 + (uint32_t)(8 * k * stride), 0, 0));
     };
     if (c_first < c_last) issue(c_first);
     for (int c = c_first; c < c_last; ++c) {
@@ -3731,6 +3728,11 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         // descriptors (read whether or not the gates pass) are in flight together — two dependent round
         // trips per step instead of two per candidate
         constexpr int kStU = 2;
+        // the next step's bucket slots are read with this step's records (one dependent round trip less per
+        // further step of a long bucket)
+        int nx[kStU];
+#pragma unroll
+        for (int j = 0; j < kStU; ++j) nx[j] = b + sl + 16 * j < e ? (int)bidxs[b + sl + 16 * j] : -1;
 #ifdef ORBFE_X_ST_NOSEARCH  // ablation (wrong results): no candidate loop, every keypoint matches right keypoint 0
         key = 0u;
         for (int k0 = e; k0 < e; k0 += 16 * kStU) {
@@ -3739,7 +3741,12 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
 #endif
             int iR[kStU];
 #pragma unroll
-            for (int j = 0; j < kStU; ++j) iR[j] = k0 + 16 * j < e ? (int)bidxs[k0 + 16 * j] : -1;
+            for (int j = 0; j < kStU; ++j) iR[j] = nx[j];
+#pragma unroll
+            for (int j = 0; j < kStU; ++j) {
+                const int kn = k0 + 16 * (kStU + j);
+                nx[j] = kn < e ? (int)bidxs[kn] : -1;
+            }
             float2 ri[kStU];
             uint4 b0[kStU], b1[kStU];
 #pragma unroll
