@@ -80,3 +80,22 @@ def test_gpu_push_carries_no_dev_variant_libraries():
     if LIB.exists():
         assert "./pyorbslam_amd/_lib/liborbfe.so" in names
     assert "./bench.py" in names and "./tests/golden/" in names
+
+
+def test_buffer_resources_built_only_by_the_helpers():
+    """Every buffer resource of the kernels is built by uniform_rsrc / bounded_rsrc / aligned_rsrc, which pass the
+    address halves through uint32_t: __builtin_amdgcn_readfirstlane returns int, and an ad-hoc construction that
+    OR-ed its sign-extended low half into the 64-bit base corrupted the high address bits whenever bit 31 of
+    the address was set (round 6: two GPU faults on the 4 500-px batch test)."""
+    src = (ROOT / "pyorbslam_amd" / "csrc" / "orbfe_kernels.hip").read_text()
+    helpers = {"uniform_rsrc", "bounded_rsrc", "aligned_rsrc"}
+    current, offenders = None, []
+    for i, line in enumerate(src.splitlines(), 1):
+        m = re.match(r"^__device__ __forceinline__ __amdgpu_buffer_rsrc_t (\w+)\(", line)
+        if m:
+            current = m.group(1)
+        elif re.match(r"^\S", line):
+            current = None
+        if "__builtin_amdgcn_make_buffer_rsrc" in line and current not in helpers:
+            offenders.append(i)
+    assert not offenders, f"buffer resources built outside the helpers at lines {offenders}"
