@@ -61,7 +61,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t aligned_rsrc(const void* p, ui
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     *bias = lo & 3u;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | (lo & ~3u)), 0, nbytes + (lo & 3u),
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(nbytes);  // wave-uniform: an SGPR resource, never waterfalled
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | (lo & ~3u)), 0, nb + (lo & 3u),
                                              0x00020000);
 }
 
@@ -3629,7 +3630,7 @@ __device__ __forceinline__ void sheared_pos(int w, int r, int c0, int& pr, int& 
     pc = f - pr * pw;
 }
 
-// n consecutive pixels of the sheared view from padded (pr, pc) as NDW dwords (byte j of the run = byte j % 4 of
+// n consecutive pixels (row r, columns c0 ..) of the sheared view as NDW dwords (byte j of the run = byte j % 4 of
 // w[j / 4]; n + 3 <= 4 NDW: the left patch's 11 bytes in 4 dwords, the right strip's 21 in 6), when the run
 // lies inside the level (returns false otherwise: a border row, whose bytes k_stereo gathers lane-parallel).
 // The loads are one dwordx4 (+ one dwordx2): 2 memory instructions per row instead of 6 dword loads (VERDICT r5
@@ -3641,8 +3642,10 @@ __device__ __forceinline__ void sheared_pos(int w, int r, int c0, int& pr, int& 
 // k_stereo masks them.
 template <int NDW>
 __device__ __forceinline__ bool sheared_words(__amdgpu_buffer_rsrc_t rs, uint32_t bias, uint32_t lvl_off, int stride,
-                                              int w, int h, int pr, int pc, int n, uint32_t (&wd)[NDW]) {
+                                              int w, int h, int r, int c0, int n, uint32_t (&wd)[NDW]) {
     static_assert(NDW == 4 || NDW == 6, "4 or 6 dwords");
+    int pr, pc;
+    sheared_pos(w, r, c0, pr, pc);
     if (!(pr >= kEdge && pr < kEdge + h && pc >= kEdge && pc + n <= kEdge + w)) return false;
     const uint32_t off = bias + lvl_off + (uint32_t)((pr - kEdge) * stride + (pc - kEdge));
     const uint32_t sh = off & 3u, al = off - sh;
@@ -3788,7 +3791,7 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
     // a window row that reaches the level's reflected border (or wraps into the next padded row): its padded
     // (row, column) start, for the lane-parallel gather below
     bool bdl = false, bdr = false;
-    int prl = 0, pcl = 0, prr = 0, pcr = 0;
+    int wrow = 0, c0l = 0, c0r = 0;  // this lane's window row and the two windows' first columns
     if (refine) {
         const int oct = kl.octave;
         const double isf = (double)s_isc[oct];
@@ -3806,15 +3809,23 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
 #endif
         if (do_sad && sl < 11) {  // lane sl stages window row sl
             uint32_t wl[4], wr[6];
-            sheared_pos(lw, scaledvL - 5 + sl, scaleduL - 5, prl, pcl);
-            sheared_pos(lw, scaledvL - 5 + sl, scaleduR0 - 10, prr, pcr);
-            if (oct == 0) {
-                bdl = !sheared_words(rsL0, bL0, 0u, lstride, lw, lh, prl, pcl, 11, wl);
-                bdr = !sheared_words(rsR0, bR0, 0u, lstride, lw, lh, prr, pcr, 21, wr);
-            } else {
-                const uint32_t lo = (uint32_t)s_wsoff[oct];
-                bdl = !sheared_words(rsLW, bLW, lo, lstride, lw, lh, prl, pcl, 11, wl);
-                bdr = !sheared_words(rsRW, bRW, lo, lstride, lw, lh, prr, pcr, 21, wr);
+            wrow = scaledvL - 5 + sl;
+            c0l = scaleduL - 5;
+            c0r = scaleduR0 - 10;
+            // one pass per distinct octave among the active lanes (nearly always one), each with wave-uniform
+            // resources: a resource selected per lane makes the compiler waterfall every window load
+            for (;;) {
+                const int ou = __builtin_amdgcn_readfirstlane(oct);
+                if (oct == ou) {
+                    const bool z = ou == 0;
+                    const uint32_t lo = z ? 0u : (uint32_t)s_wsoff[oct];
+                    uint32_t bl, br;
+                    const __amdgpu_buffer_rsrc_t rl = aligned_rsrc(z ? lvl0L : wsL, z ? img_bytes : (uint32_t)g.ws_bytes, &bl);
+                    const __amdgpu_buffer_rsrc_t rr = aligned_rsrc(z ? lvl0R : wsR, z ? img_bytes : (uint32_t)g.ws_bytes, &br);
+                    bdl = !sheared_words(rl, bl, lo, lstride, lw, lh, wrow, c0l, 11, wl);
+                    bdr = !sheared_words(rr, br, lo, lstride, lw, lh, wrow, c0r, 21, wr);
+                    break;
+                }
             }
             constexpr uint32_t k512 = 0x02000200u;
             // bytes (b, b + 1) of a dword pair as two u16 (0x0c selects a zero byte)
@@ -3844,62 +3855,51 @@ __global__ __launch_bounds__(256) void k_stereo(Geo g, StereoArgs A) {
         }
     }
     // Border rows (reflect-101 bytes of the padded level, or a run wrapping into the next padded row): 4-14 % of
-    // the window rows on KITTI levels, but in most refining waves.  Up to kStB rows per pass, each row's n bytes
-    // gathered by lanes 0 .. n - 1 of the wave (the row, its level and its image wave-uniform from the owning
-    // lane), all the pass's byte loads in flight before its first store (one memory round trip per pass), each
-    // byte stored as its u16 (pixel + 512) entry of the staged window; bytes past n stay unwritten (the SAD
-    // masks them).  A per-lane byte loop over its own row made every wave with one border row run 34
-    // dependent-address byte loads per lane.
+    // the window rows on KITTI levels, but in most refining waves.  Up to three rows per pass, one per 21-lane
+    // slot of the wave (lane 21 k + j takes byte j of the pass's row k: its padded start, level and image from
+    // the owning lane through ds_bpermute, the byte through a global load at its own address), each byte stored
+    // as its u16 (pixel + 512) entry of the staged window; bytes past n stay unwritten (the SAD masks them).
+    // A per-lane byte loop over its own row made every wave with one border row run 34 dependent-address byte
+    // loads per lane (stereo 541 -> 534 us with one row per pass, this form below).
     {
-        constexpr int kStB = 4;
         uint64_t mL = __ballot(bdl), mR = __ballot(bdr);
+        const int slot = lane / 21, jb = lane - 21 * slot;  // slot 3 (lane 63) idles
         while (mL | mR) {
-            uint32_t v[kStB];
-            int own[kStB];
-            bool rt[kStB], ok[kStB];
-            // branch-free per row (a resource chosen by branches made the compiler wait for each row's load at
-            // the join): the row's buffer selected as a wave-uniform pointer, every lane loads (lanes past n
-            // repeat byte n - 1; a pass slot without a row reads lane 0's, harmlessly: bounds-checked)
+            int own = 0;
+            bool rt = false, ok = false;
 #pragma unroll
-            for (int u = 0; u < kStB; ++u) {
-                ok[u] = (mL | mR) != 0;
-                rt[u] = mR != 0;
-                const uint64_t m = rt[u] ? mR : mL;
-                own[u] = ok[u] ? __builtin_ctzll(m) : 0;
-                if (rt[u]) mR &= mR - 1;
+            for (int k = 0; k < 3; ++k) {  // the pass's rows, right windows first (wave-uniform)
+                const bool okk = (mL | mR) != 0, rtk = mR != 0;
+                const int ownk = okk ? __builtin_ctzll(rtk ? mR : mL) : 0;
+                if (rtk) mR &= mR - 1;
                 else mL &= mL - 1;
-                const int pr0 = __builtin_amdgcn_readlane(rt[u] ? prr : prl, own[u]);
-                const int pc0 = __builtin_amdgcn_readlane(rt[u] ? pcr : pcl, own[u]);
-                const int oct = __builtin_amdgcn_readlane(kl.octave, own[u]);
-                // the level's geometry as SGPRs (an LDS read is not known to be uniform: a resource built from
-                // it would be waterfalled)
-                const int w = __builtin_amdgcn_readfirstlane(s_w[oct]), h = __builtin_amdgcn_readfirstlane(s_h[oct]);
-                const int pw = w + 2 * kEdge;
-                const int stride = oct == 0 ? g.W : __builtin_amdgcn_readfirstlane(s_pitch[oct]);
-                const uint32_t lo = oct == 0 ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)s_wsoff[oct]);
-                const uint8_t* base = oct == 0 ? (rt[u] ? lvl0R : lvl0L) : (rt[u] ? wsR : wsL);
-                uint32_t bias;
-                const __amdgpu_buffer_rsrc_t rs = aligned_rsrc(base, oct == 0 ? img_bytes : (uint32_t)g.ws_bytes, &bias);
-                int c = pc0 + min(lane, rt[u] ? 20 : 10), r = pr0;
+                if (slot == k) {
+                    own = ownk;
+                    rt = rtk;
+                    ok = okk;
+                }
+            }
+            const int orow = __shfl(wrow, own, 64), ocl = __shfl(c0l, own, 64), ocr = __shfl(c0r, own, 64);
+            const int oct = __shfl(kl.octave, own, 64);
+            if (ok && jb < (rt ? 21 : 11)) {
+                const int w = s_w[oct], h = s_h[oct], pw = w + 2 * kEdge;
+                const int stride = oct == 0 ? g.W : s_pitch[oct];
+                int r, c;
+                sheared_pos(w, orow, rt ? ocr : ocl, r, c);
+                c += jb;
                 if (c >= pw) {
                     c -= pw;
                     ++r;
                 }
-                const uint32_t off = (uint32_t)(reflect101(r - kEdge, h) * stride + reflect101(c - kEdge, w));
-                v[u] = __builtin_amdgcn_raw_buffer_load_b8(rs, bias + lo + off, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < kStB; ++u) {
-                if (ok[u] && lane < (rt[u] ? 21 : 11)) {
-                    const uint16_t e = (uint16_t)(v[u] + 512u);
-                    // the owner's group in the block
-                    const int gq = (int)(threadIdx.x >> 6) * 4 + (own[u] >> 4), gs = own[u] & 15;
-                    if (rt[u]) {
-                        ((uint16_t*)&sE[gq][gs][0])[lane] = e;
-                        if (lane >= 1) ((uint16_t*)&sO[gq][gs][0])[lane - 1] = e;
-                    } else {
-                        ((uint16_t*)&sP[gq][gs][0])[lane] = e;
-                    }
+                const uint8_t* base = oct == 0 ? (rt ? lvl0R : lvl0L) : (rt ? wsR : wsL) + s_wsoff[oct];
+                const uint16_t e = (uint16_t)(base[(int64_t)reflect101(r - kEdge, h) * stride + reflect101(c - kEdge, w)] + 512u);
+                // the owner's group in the block
+                const int gq = (int)(threadIdx.x >> 6) * 4 + (own >> 4), gs = own & 15;
+                if (rt) {
+                    ((uint16_t*)&sE[gq][gs][0])[jb] = e;
+                    if (jb >= 1) ((uint16_t*)&sO[gq][gs][0])[jb - 1] = e;
+                } else {
+                    ((uint16_t*)&sP[gq][gs][0])[jb] = e;
                 }
             }
         }
